@@ -1,0 +1,283 @@
+/*
+ * pktgpu.h — C ABI of the MI355X-native batched packet-header parser.
+ *
+ * This is the drop-in boundary for packet_rs 0.4.0's decode path:
+ *   - the protocol walk `parser::fast::parse` and its 17 sub-entries
+ *     (reference src/parser/fast.rs:5-227),
+ *   - the `make_header!` MSB-first bit-field getters of the Slice headers
+ *     (reference src/headers.rs:195-201 getters, 202-211 bytes(), 252-263 bit_range,
+ *      field tables 529-827),
+ *   - `Packet::ipv4_checksum` (reference src/packet.rs:93-107, incl. its carry-fold quirk).
+ *
+ * The reference is a Rust crate with no FFI of its own; these entry points are what a
+ * Rust `extern "C"` block binds in place of calling
+ * `fast::parse(&[u8]) -> PacketSlice` once per packet.  Everything here is plain C:
+ * pointers, sizes and status codes.  No HIP, torch or C++ types cross the boundary
+ * (streams are passed as `void*` = hipStream_t, 0 = the null stream).
+ *
+ * Errors: every function returns an int, 0 on success and a negative PKT_ERR_* code
+ * otherwise.  Nothing panics or aborts across the ABI (the reference panics on short
+ * input, fast.rs:6 and every `&arr[0..X::size()]`; here that is a per-packet
+ * PKT_TRUNCATED status instead).
+ */
+#ifndef PKTGPU_H
+#define PKTGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PKTGPU_ABI_VERSION 1
+
+/* Maximum number of headers recorded per packet.  The reference recursion is unbounded
+ * (fast.rs:53 VLAN stacks, :69 MPLS stacks, :89/:92/:104/:107 IP-in-IP, :168/:186/:219
+ * tunnels back to Ethernet); chains longer than this report PKT_DEPTH_LIMIT. */
+#define PKT_MAX_HDRS 16
+
+/* Call-level return codes. */
+#define PKT_SUCCESS            0
+#define PKT_ERR_INVALID_ARG   -1
+#define PKT_ERR_HIP           -2
+#define PKT_ERR_NO_DEVICE     -3
+#define PKT_ERR_UNSUPPORTED   -4
+
+/* Per-packet status (out->status). */
+typedef enum pkt_status {
+    PKT_OK          = 0, /* walk reached `accept` (fast.rs:223-227) */
+    PKT_TRUNCATED   = 1, /* the reference would panic on a slice index (Q7) */
+    PKT_DEPTH_LIMIT = 2  /* more than PKT_MAX_HDRS headers (build-only bound) */
+} pkt_status_t;
+
+/* Header type ids.  Names (pkt_hdr_name) are the reference's `Header::name()` strings,
+ * i.e. the make_header! identifiers of headers.rs:529-827. */
+typedef enum pkt_hdr_type {
+    PKT_HDR_NONE               = 0,
+    PKT_HDR_ETHER              = 1,  /* headers.rs:530-540  14 B */
+    PKT_HDR_VLAN               = 2,  /* headers.rs:543-552   4 B */
+    PKT_HDR_IPV4               = 3,  /* headers.rs:555-574  20 B */
+    PKT_HDR_IPV6               = 4,  /* headers.rs:577-592  40 B */
+    PKT_HDR_ICMP               = 5,  /* headers.rs:595-603   4 B */
+    PKT_HDR_TCP                = 6,  /* headers.rs:606-622  20 B */
+    PKT_HDR_UDP                = 7,  /* headers.rs:625-634   8 B */
+    PKT_HDR_ARP                = 8,  /* headers.rs:637-653  28 B */
+    PKT_HDR_VXLAN              = 9,  /* headers.rs:656-665   8 B */
+    PKT_HDR_DOT3               = 10, /* headers.rs:668-678  14 B */
+    PKT_HDR_LLC                = 11, /* headers.rs:681-689   3 B */
+    PKT_HDR_SNAP               = 12, /* headers.rs:692-699   5 B */
+    PKT_HDR_GRE                = 13, /* headers.rs:702-716   4 B */
+    PKT_HDR_GRE_CHKSUM_OFFSET  = 14, /* headers.rs:719-726   4 B */
+    PKT_HDR_GRE_SEQUENCE_NUM   = 15, /* headers.rs:729-735   4 B */
+    PKT_HDR_GRE_KEY            = 16, /* headers.rs:738-744   4 B */
+    PKT_HDR_ERSPAN2            = 17, /* headers.rs:747-760   8 B */
+    PKT_HDR_ERSPAN3            = 18, /* headers.rs:763-782  12 B */
+    PKT_HDR_ERSPAN_PLATFORM    = 19, /* headers.rs:785-792   8 B */
+    PKT_HDR_STP                = 20, /* headers.rs:795-815  35 B (never produced by the walk) */
+    PKT_HDR_MPLS               = 21, /* headers.rs:818-827   4 B */
+    PKT_HDR_COUNT              = 22
+} pkt_hdr_type_t;
+
+/* Entry points: one per public function of parser::fast (fast.rs).  Parsing a batch with
+ * entry E is `fast::parse_E(&pkt[..])` for every packet. */
+typedef enum pkt_entry {
+    PKT_ENTRY_PARSE     = 0,  /* fast::parse          fast.rs:5   (Dot3 if bytes 12..13 < 1500) */
+    PKT_ENTRY_DOT3      = 1,  /* fast::parse_dot3     fast.rs:13  */
+    PKT_ENTRY_LLC       = 2,  /* fast::parse_llc      fast.rs:19  */
+    PKT_ENTRY_SNAP      = 3,  /* fast::parse_snap     fast.rs:29  */
+    PKT_ENTRY_ETHERNET  = 4,  /* fast::parse_ethernet fast.rs:35  */
+    PKT_ENTRY_VLAN      = 5,  /* fast::parse_vlan     fast.rs:49  */
+    PKT_ENTRY_MPLS      = 6,  /* fast::parse_mpls     fast.rs:63  */
+    PKT_ENTRY_MPLS_BOS  = 7,  /* fast::parse_mpls_bos fast.rs:74  */
+    PKT_ENTRY_IPV4      = 8,  /* fast::parse_ipv4     fast.rs:84  */
+    PKT_ENTRY_IPV6      = 9,  /* fast::parse_ipv6     fast.rs:99  */
+    PKT_ENTRY_GRE       = 10, /* fast::parse_gre      fast.rs:114 */
+    PKT_ENTRY_ERSPAN2   = 11, /* fast::parse_erspan2  fast.rs:166 */
+    PKT_ENTRY_ERSPAN3   = 12, /* fast::parse_erspan3  fast.rs:172 */
+    PKT_ENTRY_ARP       = 13, /* fast::parse_arp      fast.rs:193 */
+    PKT_ENTRY_ICMP      = 14, /* fast::parse_icmp     fast.rs:198 */
+    PKT_ENTRY_TCP       = 15, /* fast::parse_tcp      fast.rs:203 */
+    PKT_ENTRY_UDP       = 16, /* fast::parse_udp      fast.rs:208 */
+    PKT_ENTRY_VXLAN     = 17, /* fast::parse_vxlan    fast.rs:218 */
+    PKT_ENTRY_COUNT     = 18
+} pkt_entry_t;
+
+/* A batch of packets resident in device memory (the caller owns every buffer).
+ *  - Fixed-stride slab: offsets == NULL; packet i starts at slab + i*stride.  Its length is
+ *    lens[i] when lens != NULL, else `stride`.
+ *  - Indexed slab (e.g. a pcap file copied as-is): offsets[i] / lens[i] (both required)
+ *    give each packet's byte range inside the slab.
+ * The slab pointer must be 16-byte aligned; the kernels may read up to 15 bytes past a
+ * packet's end but never past round_up(slab + slab_len, 16) (always inside a hipMalloc /
+ * torch allocation, whose granularity is >= 256 B). */
+typedef struct pkt_batch {
+    const uint8_t  *slab;      /* device */
+    uint64_t        slab_len;  /* bytes */
+    const uint64_t *offsets;   /* device, [n] or NULL */
+    const uint32_t *lens;      /* device, [n] or NULL */
+    uint32_t        stride;    /* bytes between packets when offsets == NULL */
+    uint32_t        reserved;
+    uint64_t        n;         /* number of packets */
+} pkt_batch_t;
+
+/* Output columns (struct-of-arrays, device memory, caller-owned).  Every pointer may be
+ * NULL: that column is then neither computed nor written (the reference's getters are
+ * lazy, headers.rs:195-201 — a caller asks only for what it reads).
+ *
+ * Chain columns = PacketSlice (lib.rs:136-140, packet.rs:714-761):
+ *   hdr_type/hdr_off are slot-major: slot j of packet i lives at [j*n + i]; only slots
+ *   j < n_hdrs[i] are written.  List order is the reference's `Vec::insert(0, ..)` order,
+ *   i.e. wire order except GRE options (Q2: GRE, SeqNum, Key, ChksumOffset).
+ *   hdr_off is the header's byte offset from the start of the packet (the Slice's
+ *   pointer, headers.rs:187-192); payload_off/payload_len = PacketSlice::payload().
+ *   On PKT_TRUNCATED / PKT_DEPTH_LIMIT no PacketSlice exists (the reference panics):
+ *   n_hdrs = 0, hdr_mask = 0, payload_off = payload_len = 0 and every field column is 0.
+ *
+ * Field columns = the Slice getters of the FIRST header of that type in the list
+ * (Packet's Index<&str> returns the first match, packet.rs:64-66 — Q11).  Values are the
+ * reference's u64 getter results narrowed to the field's natural width; 0 when the packet
+ * has no such header (check hdr_mask).  ipv6_src/dst are the 16 raw bytes that
+ * `bytes(msb, lsb)` returns (headers.rs:202-211; the u64 getter is Q8).
+ * ipv4_csum_calc = Packet::ipv4_checksum over that IPv4 header's 20 bytes (packet.rs:93-107). */
+typedef struct pkt_out {
+    /* chain */
+    uint8_t  *status;          /* pkt_status_t */
+    uint8_t  *n_hdrs;
+    uint8_t  *hdr_type;        /* [PKT_MAX_HDRS][n] */
+    uint16_t *hdr_off;         /* [PKT_MAX_HDRS][n] */
+    uint16_t *payload_off;
+    uint16_t *payload_len;
+    uint32_t *hdr_mask;        /* bit t set iff a header of type t is in the list */
+    /* Ether (headers.rs:530-540) */
+    uint64_t *eth_dst;
+    uint64_t *eth_src;
+    uint16_t *eth_etype;
+    /* Vlan (headers.rs:543-552) */
+    uint8_t  *vlan_pcp;
+    uint8_t  *vlan_cfi;
+    uint16_t *vlan_vid;
+    uint16_t *vlan_etype;
+    /* IPv4 (headers.rs:555-574) */
+    uint8_t  *ipv4_version;
+    uint8_t  *ipv4_ihl;
+    uint8_t  *ipv4_diffserv;
+    uint16_t *ipv4_total_len;
+    uint16_t *ipv4_identification;
+    uint8_t  *ipv4_flags;
+    uint16_t *ipv4_frag_startset;
+    uint8_t  *ipv4_ttl;
+    uint8_t  *ipv4_protocol;
+    uint16_t *ipv4_header_checksum;
+    uint32_t *ipv4_src;
+    uint32_t *ipv4_dst;
+    uint16_t *ipv4_csum_calc;  /* Packet::ipv4_checksum (packet.rs:93-107) */
+    /* IPv6 (headers.rs:577-592) */
+    uint8_t  *ipv6_version;
+    uint8_t  *ipv6_traffic_class;
+    uint32_t *ipv6_flow_label;
+    uint16_t *ipv6_payload_len;
+    uint8_t  *ipv6_next_hdr;
+    uint8_t  *ipv6_hop_limit;
+    uint8_t  *ipv6_src;        /* [n][16] */
+    uint8_t  *ipv6_dst;        /* [n][16] */
+    /* TCP (headers.rs:606-622) */
+    uint16_t *tcp_src;
+    uint16_t *tcp_dst;
+    uint32_t *tcp_seq_no;
+    uint32_t *tcp_ack_no;
+    uint8_t  *tcp_data_startset;
+    uint8_t  *tcp_res;
+    uint8_t  *tcp_flags;
+    uint16_t *tcp_window;
+    uint16_t *tcp_checksum;
+    uint16_t *tcp_urgent_ptr;
+    /* UDP (headers.rs:625-634) */
+    uint16_t *udp_src;
+    uint16_t *udp_dst;
+    uint16_t *udp_length;
+    uint16_t *udp_checksum;
+} pkt_out_t;
+
+/* A field request for pkt_extract_fields: bits [start..=end] (MSB-first from the header's
+ * first byte, the make_header! convention) of the `occurrence`-th header of `hdr_type`
+ * in the chain (0 = first, as Packet's Index<&str>).  Any bit range is allowed, so a
+ * user-defined make_header! field (lib.rs:81-103) is extracted the same way.  Widths
+ * above 64 bits follow bit_range's release-build result (headers.rs:262, Q8). */
+typedef struct pkt_field_spec {
+    uint8_t  hdr_type;
+    uint8_t  occurrence;
+    uint16_t start;
+    uint16_t end;
+    uint16_t reserved;
+} pkt_field_spec_t;
+
+/* Chain columns produced by pkt_parse_batch, as input to pkt_extract_fields. */
+typedef struct pkt_chain {
+    const uint8_t  *n_hdrs;    /* [n] */
+    const uint8_t  *hdr_type;  /* [PKT_MAX_HDRS][n] */
+    const uint16_t *hdr_off;   /* [PKT_MAX_HDRS][n] */
+} pkt_chain_t;
+
+typedef struct pkt_ctx pkt_ctx_t;
+
+/* ---- metadata (host only, no device needed) ---- */
+int         pkt_abi_version(void);
+/* sizeof the ABI structs, so a foreign binding (Rust/ctypes) can check its layout. */
+size_t      pkt_sizeof_batch(void);
+size_t      pkt_sizeof_out(void);
+size_t      pkt_sizeof_field_spec(void);
+/* Header::name() (headers.rs:218-220); NULL for an unknown id. */
+const char *pkt_hdr_name(int hdr_type);
+/* <Hdr>::size() (headers.rs:212-214); 0 for an unknown id. */
+int         pkt_hdr_size(int hdr_type);
+/* Field table of a header type (make_header! field list, headers.rs:529-827). */
+int         pkt_hdr_field_count(int hdr_type);
+int         pkt_hdr_field(int hdr_type, int idx, const char **name, uint16_t *start, uint16_t *end);
+const char *pkt_status_name(int status);
+const char *pkt_entry_name(int entry);   /* "parse", "parse_ethernet", ... */
+
+/* ---- context ---- */
+/* Binds to HIP device `device`.  No per-call allocation happens after creation. */
+int         pkt_ctx_create(int device, pkt_ctx_t **ctx);
+int         pkt_ctx_destroy(pkt_ctx_t *ctx);
+const char *pkt_ctx_last_error(const pkt_ctx_t *ctx);
+/* Tuning knob: packets staged per wave window (bytes of each packet copied to LDS).
+ * 0 = automatic.  Values are rounded to a multiple of 16 and clamped to [16, 256]. */
+int         pkt_ctx_set_window(pkt_ctx_t *ctx, uint32_t window_bytes);
+
+/* ---- the hot path ---- */
+/* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
+ * Asynchronous on `stream`; returns after the launch. */
+int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
+                    const pkt_out_t *out, void *stream);
+
+/* Batched make_header! getter: for each spec s and packet i, values[s][i] = the field of
+ * the chain's matching header (0 and found[s][i] = 0 when absent).  `values` and `found`
+ * are HOST arrays of `nspec` DEVICE pointers, each to n elements; found may be NULL and
+ * so may any found[s]. */
+int pkt_extract_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
+                       const pkt_field_spec_t *specs, uint32_t nspec,
+                       uint64_t *const *values, uint8_t *const *found, void *stream);
+
+/* Packet::ipv4_checksum (packet.rs:93-107) over n headers of 20 bytes at a fixed stride
+ * in device memory: out[i] = checksum(hdrs + i*stride). */
+int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride, uint64_t n,
+                            uint16_t *out, void *stream);
+
+/* ---- host-side helpers ---- */
+/* Index a pcap byte buffer in the tests/pcap.rs:7-37 format (LE magic d4 c3 b2 a1, 24-byte
+ * global header, 16-byte record headers).  Writes up to `cap` record (data offset, incl_len)
+ * pairs and the record count to *n_out (which can exceed cap: call again with a larger cap).
+ * Returns PKT_ERR_INVALID_ARG on a bad magic or a record running past `len`. */
+int pkt_pcap_index(const uint8_t *buf, uint64_t len, uint64_t *offsets, uint32_t *lens,
+                   uint64_t cap, uint64_t *n_out);
+
+/* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
+uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PKTGPU_H */
