@@ -1,0 +1,251 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident batched parse of packet slabs on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+A step = one pkt_parse_batch launch over one batch of 2^20 packets (config C2 by default:
+64-byte Ether/IPv4/UDP, fixed stride) producing the chain + Ether/IPv4/UDP field tuple +
+recomputed IPv4 checksum.  Each step reads a different slab of a >= 1 GiB ring (and writes a
+different output set), so the 256 MiB Infinity Cache cannot serve the working set.  Inputs are
+resident in HBM before the timed region starts.
+
+Multi-GPU (one process per GPU): every rank parses its own batch (weak scaling, no collective
+in the step); after the timed loop the per-packet tuples of one step are gathered to rank 0
+with RCCL and timed separately ("gather" in the JSON line).
+
+Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "packet-rs_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def parse_args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU per step")
+    ap.add_argument("--ring-gib", type=float, default=1.0)
+    ap.add_argument("--columns", default="chain,ether,ipv4,udp")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    return ap.parse_args()
+
+
+def make_input(cfg, n, seed):
+    from pktgpu import gen
+    if cfg == "c2":
+        return gen.gen_c2(n, seed=seed).reshape(-1), 64, None, None
+    if cfg == "c3":
+        return gen.gen_c3(n, seed=seed).reshape(-1), 128, None, None
+    buf, offs, lens = gen.gen_c4(n, seed=seed)
+    return buf, None, offs, lens
+
+
+def algorithmic_bytes(n, cols, n_slots, span):
+    """read = sum over packets of ceil64(header span) — the 64-byte request granularity of the
+    bytes the walk must see (span = offset of the payload, i.e. the end of the last header);
+    written = bytes of the requested output columns (slot columns: the slots used)."""
+    from pktgpu import schema
+    span = np.maximum(span.astype(np.int64), 1)
+    read = int(((span + 63) // 64 * 64).sum())
+    written = schema.bytes_per_packet(cols, n_slots=n_slots) * n
+    return read, written
+
+
+def cpu_baseline(slab, stride, offs, lens, n, cols, threads):
+    """The oracle (C restatement of packet_rs fast::parse + getters + ipv4_checksum, with the
+    reference's per-header allocation and per-bit loops) on the host cores, bounded sample."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle
+    oracle.build()
+    reps = 4
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        oracle.parse_batch(slab, n, stride=stride, offsets=offs, lens=lens, columns=cols,
+                           nthreads=threads)
+    dt = time.perf_counter() - t0
+    n1 = min(n, 1 << 19)
+    t1 = time.perf_counter()
+    oracle.parse_batch(slab, n1, stride=stride, offsets=offs[:n1] if offs is not None else None,
+                       lens=lens[:n1] if lens is not None else None, columns=cols, nthreads=1)
+    dt1 = time.perf_counter() - t1
+    return {"value": round(reps * n / dt / 1e9, 6), "unit": "Gpkt/s", "cores": threads,
+            "kind": "port",
+            "sample": f"{reps} passes over the same {n}-packet slab ({reps * n} packets), "
+                      f"{threads} threads, oracle/pkt_oracle.c -O2 (C restatement of packet_rs "
+                      f"0.4.0 fast::parse + getters + ipv4_checksum)",
+            "single_thread_gpkt_s": round(n1 / dt1 / 1e9, 6)}
+
+
+def main():
+    args = parse_args()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    import pktgpu
+    from pktgpu import schema
+    P = pktgpu.Parser(local)
+    cols = pktgpu.resolve_columns(args.columns.split(","))
+    n = args.packets
+
+    # ---------------- input: one seeded batch per rank, replicated over a >= ring_gib ring
+    slab_np, stride, offs_np, lens_np = make_input(args.config, n, seed=0x5EED0000 + 2 + rank)
+    slab_bytes = slab_np.size
+    ring = max(2, int(np.ceil(args.ring_gib * (1 << 30) / slab_bytes)))
+    d_first = torch.from_numpy(slab_np).to(dev)
+    slabs = [d_first] + [d_first.clone() for _ in range(ring - 1)]
+    d_offs = torch.from_numpy(offs_np).to(dev) if offs_np is not None else None
+    d_lens = torch.from_numpy(lens_np).to(dev) if lens_np is not None else None
+
+    # output ring: every slot's columns are views of ONE contiguous buffer (gatherable)
+    def alloc_packed():
+        sizes, total = [], 0
+        for c in cols:
+            shp = schema.column_shape(c, n)
+            nb = int(np.prod(shp)) * schema.column_dtype(c).itemsize
+            sizes.append((c, shp, nb, total))
+            total += (nb + 255) // 256 * 256
+        buf = torch.empty(total, dtype=torch.uint8, device=dev)
+        views = {}
+        for c, shp, nb, o in sizes:
+            views[c] = buf[o:o + nb].view(pktgpu._tdtype(schema.column_dtype(c))).view(shp)
+        return buf, views
+
+    outs = [alloc_packed() for _ in range(ring)]
+    entry = schema.ENTRY_ID["parse"]
+    batches, ostructs = [], []
+    for r in range(ring):
+        b = P._batch(slabs[r], n, stride, d_offs, d_lens)
+        batches.append(b)
+        ostructs.append(P.out_struct(outs[r][1]))
+    stream = torch.cuda.current_stream(dev)
+
+    def step(k):
+        P.launch(batches[k % ring], entry, ostructs[k % ring], stream)
+
+    for k in range(args.warmup):
+        step(k)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+
+    # ---------------- timed region: K steps; per-launch HIP events on the launch stream
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        ev[k][0].record(stream)
+        step(args.warmup + k)
+        ev[k][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_ms = np.array([a.elapsed_time(b) for a, b in ev])
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---------------- gather of one step's tuples to rank 0 (N > 1), timed separately
+    gather = None
+    if world > 1:
+        buf = outs[0][0]
+        glist = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
+        dist.gather(buf, glist, dst=0)  # warm
+        torch.cuda.synchronize()
+        reps = 5
+        dist.barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        for _ in range(reps):
+            dist.gather(buf, glist, dst=0)
+        torch.cuda.synchronize()
+        dist.barrier()
+        gms = (time.perf_counter() - tg) / reps * 1e3
+        gbytes = buf.numel() * (world - 1)
+        gather = {"ms": round(gms, 4), "bytes_into_root": gbytes,
+                  "GB/s": round(gbytes / (gms * 1e-3) / 1e9, 2), "backend": "nccl(RCCL)",
+                  "packets": n * world}
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    o0 = outs[(args.warmup + args.steps - 1) % ring][1]
+    used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
+    if "payload_off" in o0:
+        span = o0["payload_off"].cpu().numpy()
+    else:
+        span = np.full(n, 64, np.int64)
+    read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
+    algo = read_b + write_b
+    avg_kern_s = float(np.mean(kern_ms)) * 1e-3
+    achieved = algo / avg_kern_s / 1e9
+    pkts_total = n * world * args.steps
+    value = pkts_total / elapsed / 1e9
+    res = {
+        "metric": "Gpkt/s + GB/s device-resident parse, 1M×64B Ether/IPv4/UDP, 1/2/4/8 MI355X",
+        "value": round(value, 4),
+        "unit": "Gpkt/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded generator, pktgpu/gen.py)",
+        "config": {
+            "workload": {"c2": "C2: 2^20 x 64 B Ether/IPv4/UDP fixed-stride slab per GPU",
+                         "c3": "C3: 2^20 x 128 B Ether/{0-2}xVlan/IPv4/TCP|UDP per GPU",
+                         "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}[args.config],
+            "packets_per_gpu": n, "entry": "fast::parse", "columns": args.columns,
+            "ring_slabs": ring, "ring_bytes": ring * slab_bytes, "parallelism": f"dp{world}",
+        },
+        "GB/s": {"algorithmic": round(algo * world * args.steps / elapsed / 1e9, 2),
+                 "slab": round(slab_bytes * world * args.steps / elapsed / 1e9, 2),
+                 "algorithmic_bytes_per_pkt": {"read": read_b / n, "written": write_b / n}},
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "kernel": "parse_kernel", "avg_kernel_us": round(avg_kern_s * 1e6, 3),
+                     "min_kernel_us": round(float(np.min(kern_ms)) * 1e3, 3),
+                     "read_only_frac": round(read_b / avg_kern_s / 1e9 / HBM_PEAK_GBS, 4)},
+    }
+    if gather is not None:
+        res["gather"] = gather
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(slab_np, stride, offs_np, lens_np, n, cols,
+                                           min(args.cpu_threads, os.cpu_count() or 1))
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

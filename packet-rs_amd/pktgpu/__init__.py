@@ -1,0 +1,285 @@
+"""pktgpu — MI355X batched packet-header parser (Python host side).
+
+Mirrors packet_rs's decode API for whole batches:
+
+    fast::parse(&[u8]) -> PacketSlice            (src/parser/fast.rs:5)
+    fast::parse_<hdr>(&[u8]) -> PacketSlice       (the 17 sub-entries, fast.rs:13-222)
+    <Hdr>Slice::<field>() -> u64                  (make_header! getters, headers.rs:195-201)
+    Packet::ipv4_checksum(&[u8]) -> u16           (src/packet.rs:93-107)
+
+    >>> import torch, pktgpu
+    >>> p = pktgpu.Parser(0)
+    >>> res = p.parse(slab_u8_cuda, stride=64)              # every column
+    >>> res = p.parse(slab, stride=64, columns=["chain", "ipv4", "udp"])
+    >>> sl = pktgpu.packet_slice(res_host, i, packet_bytes) # PacketSlice-style view
+    >>> sl.payload(), sl.to_vec(), sl["IPv4"].ttl()
+
+All compute runs in the HIP kernels of lib/libpktgpu.so through its C ABI; torch only
+provides device memory and the stream.  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from . import schema
+from .schema import (ABI_VERSION, DEPTH_LIMIT, ENTRIES, ENTRY_ID, GROUPS, HDR_ID, HDR_NAMES,  # noqa: F401
+                     HDR_SIZES, MAX_HDRS, OK, STATUS_NAMES, TRUNCATED)
+
+__all__ = ["Parser", "packet_slice", "PacketSlice", "HeaderSlice", "resolve_columns", "schema"]
+
+
+def resolve_columns(columns):
+    """"all" | list of column names and/or group names -> ordered column names."""
+    if columns is None or columns == "all":
+        return list(schema.COLUMN_NAMES)
+    if isinstance(columns, str):
+        columns = [columns]
+    out = set()
+    for c in columns:
+        if c in schema.GROUPS:
+            out.update(schema.columns_of([c]))
+        elif c in schema.COLUMN_NAMES:
+            out.add(c)
+        else:
+            raise ValueError(f"unknown column or group {c!r}")
+    return [c for c in schema.COLUMN_NAMES if c in out]
+
+
+def _torch():
+    import torch  # noqa: F401  (must be loaded before libpktgpu: shared HIP runtime)
+    return torch
+
+
+_TORCH_DT = None
+
+
+def _tdtype(np_dtype):
+    torch = _torch()
+    global _TORCH_DT
+    if _TORCH_DT is None:
+        _TORCH_DT = {np.dtype(np.uint8): torch.uint8, np.dtype(np.uint16): torch.uint16,
+                     np.dtype(np.uint32): torch.uint32, np.dtype(np.uint64): torch.uint64}
+    return _TORCH_DT[np.dtype(np_dtype)]
+
+
+class Parser:
+    """A pkt_ctx bound to one HIP device."""
+
+    def __init__(self, device=0, window=0):
+        torch = _torch()
+        from . import _lib
+        self._L = _lib.load()
+        self._lib = _lib
+        self.device = int(device)
+        self.torch_device = torch.device("cuda", self.device)
+        h = ctypes.c_void_p()
+        rc = self._L.pkt_ctx_create(self.device, ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"pkt_ctx_create({device}) failed: {rc}")
+        self._ctx = h
+        if window:
+            self._L.pkt_ctx_set_window(self._ctx, window)
+
+    def close(self):
+        if getattr(self, "_ctx", None):
+            self._L.pkt_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_window(self, window_bytes):
+        self._L.pkt_ctx_set_window(self._ctx, int(window_bytes))
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._L.pkt_ctx_last_error(self._ctx)
+            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def _stream(self, stream):
+        torch = _torch()
+        if stream is None:
+            stream = torch.cuda.current_stream(self.torch_device)
+        return ctypes.c_void_p(stream.cuda_stream)
+
+    def _batch(self, slab, n, stride, offsets, lens):
+        torch = _torch()
+        assert slab.dtype == torch.uint8 and slab.is_cuda and slab.is_contiguous()
+        b = self._lib.PktBatch()
+        b.slab = slab.data_ptr()
+        b.slab_len = slab.numel()
+        if offsets is not None:
+            assert offsets.dtype == torch.uint64 and lens is not None and lens.dtype == torch.uint32
+            b.offsets = offsets.data_ptr()
+            b.lens = lens.data_ptr()
+            n = offsets.numel() if n is None else n
+        else:
+            if lens is not None:
+                assert lens.dtype == torch.uint32
+                b.lens = lens.data_ptr()
+            if n is None:
+                n = slab.numel() // stride
+        b.stride = stride or 0
+        b.n = int(n)
+        return b
+
+    def alloc(self, n, columns="all"):
+        """Device output columns for n packets (torch tensors, uninitialised)."""
+        torch = _torch()
+        res = {}
+        for c in resolve_columns(columns):
+            res[c] = torch.empty(schema.column_shape(c, n), dtype=_tdtype(schema.column_dtype(c)),
+                                 device=self.torch_device)
+        return res
+
+    def out_struct(self, res):
+        o = self._lib.PktOut()
+        for c, t in res.items():
+            setattr(o, c, t.data_ptr() if t.numel() else None)
+        return o
+
+    def parse(self, slab, stride=None, n=None, offsets=None, lens=None, entry="parse",
+              columns="all", out=None, stream=None):
+        """fast::parse_<entry> over every packet of the slab -> {column: device tensor}."""
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        b = self._batch(slab, n, stride, offsets, lens)
+        res = out if out is not None else self.alloc(b.n, columns)
+        o = self.out_struct(res)
+        self._check(self._L.pkt_parse_batch(self._ctx, ctypes.byref(b), e, ctypes.byref(o),
+                                            self._stream(stream)), "pkt_parse_batch")
+        return res
+
+    def launch(self, batch_struct, entry, out_struct, stream=None):
+        """Relaunch with prebuilt ctypes structs (no per-call Python allocation; bench loop)."""
+        self._check(self._L.pkt_parse_batch(self._ctx, ctypes.byref(batch_struct), entry,
+                                            ctypes.byref(out_struct), self._stream(stream)),
+                    "pkt_parse_batch")
+
+    def extract_fields(self, slab, chain, specs, stride=None, n=None, offsets=None, lens=None,
+                       stream=None):
+        """Batched getter: specs = [(hdr_type|name, occurrence, start, end)] -> (values, found)."""
+        torch = _torch()
+        b = self._batch(slab, n, stride, offsets, lens)
+        ch = self._lib.PktChain()
+        ch.n_hdrs = chain["n_hdrs"].data_ptr()
+        ch.hdr_type = chain["hdr_type"].data_ptr()
+        ch.hdr_off = chain["hdr_off"].data_ptr()
+        k = len(specs)
+        sp = (self._lib.PktFieldSpec * max(1, k))()
+        for i, (t, occ, s, e) in enumerate(specs):
+            t = HDR_ID[t] if isinstance(t, str) else int(t)
+            sp[i] = self._lib.PktFieldSpec(t, occ, s, e, 0)
+        vals = [torch.empty(b.n, dtype=torch.uint64, device=self.torch_device) for _ in range(k)]
+        found = [torch.empty(b.n, dtype=torch.uint8, device=self.torch_device) for _ in range(k)]
+        vp = (ctypes.c_void_p * max(1, k))(*[v.data_ptr() for v in vals])
+        fp = (ctypes.c_void_p * max(1, k))(*[f.data_ptr() for f in found])
+        self._check(self._L.pkt_extract_fields(self._ctx, ctypes.byref(b), ctypes.byref(ch), sp, k,
+                                               vp, fp, self._stream(stream)), "pkt_extract_fields")
+        return vals, found
+
+    def ipv4_checksum(self, hdrs, stride=20, n=None, stream=None):
+        """Packet::ipv4_checksum over n 20-byte headers at a fixed stride (device u8 tensor)."""
+        torch = _torch()
+        n = hdrs.numel() // stride if n is None else n
+        out = torch.empty(n, dtype=torch.uint16, device=self.torch_device)
+        self._check(self._L.pkt_ipv4_checksum_batch(self._ctx, ctypes.c_void_p(hdrs.data_ptr()),
+                                                    stride, n, ctypes.c_void_p(out.data_ptr()),
+                                                    self._stream(stream)), "pkt_ipv4_checksum_batch")
+        return out
+
+
+def pcap_index(buf):
+    """(offsets uint64, lens uint32) of a tests/pcap.rs-format buffer, via the C ABI."""
+    from . import _lib
+    L = _lib.load()
+    a = np.ascontiguousarray(np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+    n = ctypes.c_uint64()
+    rc = L.pkt_pcap_index(a.ctypes.data, a.size, None, None, 0, ctypes.byref(n))
+    if rc != 0:
+        raise ValueError("bad pcap")
+    offs = np.zeros(n.value, np.uint64)
+    lens = np.zeros(n.value, np.uint32)
+    rc = L.pkt_pcap_index(a.ctypes.data, a.size, offs.ctypes.data, lens.ctypes.data, n.value,
+                          ctypes.byref(n))
+    if rc != 0:
+        raise ValueError("bad pcap")
+    return offs, lens
+
+
+# ----------------------------------------------------------------- PacketSlice-style host views
+class HeaderSlice:
+    """A `<Hdr>Slice` (headers.rs:172-296): a name and a view of `len()` bytes of the packet.
+    Field getters are generated from the header's make_header! table."""
+
+    def __init__(self, hdr_type, data):
+        self.hdr_type = hdr_type
+        self._data = data
+
+    def name(self):
+        return HDR_NAMES[self.hdr_type]
+
+    def len(self):
+        return HDR_SIZES[self.hdr_type]
+
+    def as_slice(self):
+        return bytes(self._data[:self.len()])
+
+    def bit_range(self, msb, lsb):
+        """headers.rs:253-263 (release semantics for widths > 64, Q8)."""
+        v = 0
+        for i in range(lsb, msb + 1):
+            v = (v << 1) | ((self._data[i // 8] >> (7 - i % 8)) & 1)
+        w = msb - lsb + 1
+        v &= (1 << 64) - 1
+        sh = (64 - w) & 63
+        return ((v << sh) & ((1 << 64) - 1)) >> sh
+
+    def bytes(self, msb, lsb):
+        return bytes(self.bit_range(i + 7, i) for i in range(lsb, msb + 1, 8))
+
+    def __getattr__(self, field):
+        from . import fields
+        rng = fields.FIELDS.get(self.hdr_type, {}).get(field)
+        if rng is None:
+            raise AttributeError(field)
+        return lambda: self.bit_range(rng[1], rng[0])
+
+
+class PacketSlice:
+    """packet_rs::PacketSlice (lib.rs:136-140, packet.rs:714-761) over one parsed packet."""
+
+    def __init__(self, hdrs, payload):
+        self.hdrs = hdrs
+        self._payload = payload
+
+    def payload(self):
+        return self._payload
+
+    def len(self):
+        return sum(h.len() for h in self.hdrs) + len(self._payload)
+
+    def to_vec(self):
+        return b"".join(h.as_slice() for h in self.hdrs) + bytes(self._payload)
+
+    def __getitem__(self, name):  # first match, like Packet's Index<&str> (packet.rs:64-66)
+        for h in self.hdrs:
+            if h.name() == name:
+                return h
+        raise KeyError(name)
+
+
+def packet_slice(res, i, pkt):
+    """Build the PacketSlice of packet i from host (numpy) result columns and its bytes."""
+    if int(res["status"][i]) != OK:
+        raise ValueError(f"packet {i}: {STATUS_NAMES[int(res['status'][i])]} (the reference panics)")
+    pkt = bytes(pkt)
+    hdrs = []
+    for j in range(int(res["n_hdrs"][i])):
+        t = int(res["hdr_type"][j, i])
+        o = int(res["hdr_off"][j, i])
+        hdrs.append(HeaderSlice(t, memoryview(pkt)[o:]))
+    po, pl = int(res["payload_off"][i]), int(res["payload_len"][i])
+    return PacketSlice(hdrs, pkt[po:po + pl])

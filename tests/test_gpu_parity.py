@@ -1,0 +1,316 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle, bit for bit.
+
+Every test calls libpktgpu's kernels on a real MI355X and compares with oracle/pkt_oracle.c
+on the same seeded input.  Slot columns (hdr_type/hdr_off) are compared for the slots the
+packet owns (j < n_hdrs); everything else is compared whole.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+import oracle  # noqa: E402
+import pyref  # noqa: E402
+from pktgpu import gen, schema  # noqa: E402
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(REPO, "tests", "golden")
+H = schema.HDR_ID
+
+
+@pytest.fixture(scope="module")
+def P():
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: -m gpu tests need an MI355X")
+    import pktgpu
+    return pktgpu.Parser(0)
+
+
+def dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def to_host(res):
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in res.items()}
+
+
+def gpu_parse(P, slab, n, stride=None, offsets=None, lens=None, entry="parse", columns="all",
+              window=0):
+    ds = dev(np.ascontiguousarray(slab, np.uint8).reshape(-1))
+    do = dev(offsets.astype(np.uint64)) if offsets is not None else None
+    dl = dev(lens.astype(np.uint32)) if lens is not None else None
+    P.set_window(window)
+    try:
+        res = P.parse(ds, stride=stride, n=n, offsets=do, lens=dl, entry=entry, columns=columns)
+        return to_host(res)
+    finally:
+        P.set_window(0)
+
+
+def compare(g, o, label=""):
+    n = len(o["status"]) if "status" in o else None
+    for k, ov in o.items():
+        gv = g[k]
+        if k in ("hdr_type", "hdr_off"):
+            nh = o["n_hdrs"].astype(np.int64)
+            valid = np.arange(schema.MAX_HDRS)[:, None] < nh[None, :]
+            bad = np.nonzero(valid & (gv != ov))
+            assert bad[0].size == 0, f"{label} {k}: first mismatch slot={bad[0][:5]} pkt={bad[1][:5]}"
+        else:
+            if not np.array_equal(gv, ov):
+                idx = np.nonzero((gv != ov).reshape(len(ov), -1).any(axis=1))[0]
+                raise AssertionError(f"{label} {k}: {idx.size} mismatches, first pkts {idx[:8]}: "
+                                     f"gpu={gv[idx[:4]]} oracle={ov[idx[:4]]}")
+    return n
+
+
+def both(P, slab, n, stride=None, offsets=None, lens=None, entry="parse", columns="all", window=0,
+         label=""):
+    import pktgpu
+    cols = pktgpu.resolve_columns(columns)
+    g = gpu_parse(P, slab, n, stride, offsets, lens, entry, cols, window)
+    o = oracle.parse_batch(slab, n, stride=stride, offsets=offsets, lens=lens, entry=entry,
+                           columns=cols, nthreads=8)
+    compare(g, o, label)
+    return g, o
+
+
+# ------------------------------------------------------------------ golden 22 packets
+def test_ref22_pcap_all_columns(P):
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    offs, lens = gen.pcap_index_py(pc)
+    slab = np.frombuffer(pc, np.uint8)
+    g, _ = both(P, slab, 22, offsets=offs, lens=lens, label="ref22")
+    import json
+    exp = json.load(open(os.path.join(GOLD, "ref22_expected.json")))
+    for i, e in enumerate(exp):
+        got = [[schema.HDR_NAMES[g["hdr_type"][j, i]], int(g["hdr_off"][j, i])]
+               for j in range(g["n_hdrs"][i])]
+        assert got == e["hdrs"], e["name"]
+        assert (g["payload_off"][i], g["payload_len"][i]) == (e["payload_off"], e["payload_len"])
+
+
+@pytest.mark.parametrize("window", [0, 16, 32, 64, 256])
+def test_ref22_windows(P, window):
+    """Small windows force the global-memory fallback of the walk and the field reads."""
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    offs, lens = gen.pcap_index_py(pc)
+    both(P, np.frombuffer(pc, np.uint8), 22, offsets=offs, lens=lens, window=window,
+         label=f"w{window}")
+
+
+def test_packet_slice_view_payload(P):
+    """tests/lib.rs:818-827 through the GPU: fast::parse(..).payload() == [0..9]."""
+    import pktgpu
+    pl = bytes(range(10))
+    v = gen.test_tcp_packet_with_payload(pl).to_vec()
+    slab = np.frombuffer(v, np.uint8)
+    g = gpu_parse(P, slab, 1, stride=len(v))
+    sl = pktgpu.packet_slice(g, 0, v)
+    assert sl.payload() == pl
+    assert sl.to_vec() == v and sl.len() == len(v)
+    assert [h.name() for h in sl.hdrs] == ["Ether", "IPv4", "TCP"]
+    assert sl["IPv4"].ttl() == 64 and sl["TCP"].dst() == 8888 and sl["Ether"].etype() == 0x800
+
+
+# ------------------------------------------------------------------ benchmark configs
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 255, 257, 4097, 1 << 16])
+def test_c2_sizes(P, n):
+    slab = gen.gen_c2(n, seed=n)
+    both(P, slab, n, stride=64, label=f"c2 n={n}")
+
+
+def test_c2_full_1m(P):
+    """Config 2 at its full size (2^20 x 64 B), every column, against the oracle."""
+    n = 1 << 20
+    slab = gen.gen_c2(n)
+    g, o = both(P, slab, n, stride=64, label="c2 1M")
+    assert (g["status"] == 0).all() and (g["n_hdrs"] == 3).all()
+    good = g["ipv4_header_checksum"] == g["ipv4_csum_calc"]
+    assert 0.98 < good.mean() < 1.0  # 1 % corrupted checksums in the generator
+
+
+def test_c3_full_1m(P):
+    n = 1 << 20
+    slab = gen.gen_c3(n)
+    g, _ = both(P, slab, n, stride=128, label="c3 1M")
+    assert set(np.unique(g["n_hdrs"])) == {3, 4, 5}
+
+
+def test_c4_pcap(P):
+    n = 1 << 16
+    buf, offs, lens = gen.gen_c4(n, seed=4)
+    both(P, buf, n, offsets=offs, lens=lens, label="c4")
+
+
+def test_c2_chain_only_and_subsets(P):
+    n = 5000
+    slab = gen.gen_c2(n, seed=9)
+    for cols in (["chain"], ["status", "payload_len"], ["ipv4_csum_calc"], ["ether", "udp"]):
+        both(P, slab, n, stride=64, columns=cols, label=str(cols))
+
+
+# ------------------------------------------------------------------ entries and edge cases
+@pytest.mark.parametrize("entry", schema.ENTRIES)
+def test_entries_random_and_templates(P, entry):
+    rng = np.random.default_rng(100 + schema.ENTRY_ID[entry])
+    pkts = [p.to_vec() for p in gen.reference_22_packets()]
+    pkts += [rng.integers(0, 256, int(rng.integers(0, 200)), dtype=np.uint8).tobytes()
+             for _ in range(3000)]
+    buf = b"".join(pkts)
+    lens = np.array([len(p) for p in pkts], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    slab = np.frombuffer(buf + bytes(16), np.uint8)
+    both(P, slab, len(pkts), offsets=offs, lens=lens, entry=entry, label=entry)
+
+
+def test_truncated_prefixes(P):
+    """Every prefix (0..len) of every template, in one fixed-stride batch with lens."""
+    pkts = [p.to_vec() for p in gen.reference_22_packets()]
+    stride = 288
+    rows, lens = [], []
+    for v in pkts:
+        for L in range(0, len(v) + 1):
+            r = np.zeros(stride, np.uint8)
+            r[:len(v)] = np.frombuffer(v, np.uint8)  # bytes past len present but not packet
+            rows.append(r)
+            lens.append(L)
+    slab = np.stack(rows)
+    lens = np.array(lens, np.uint32)
+    g, o = both(P, slab, len(lens), stride=stride, lens=lens, label="prefixes")
+    assert (g["status"] == schema.TRUNCATED).sum() > 1000
+
+
+def test_empty_batch(P):
+    import pktgpu
+    ds = dev(np.zeros(64, np.uint8))
+    res = P.parse(ds, stride=64, n=0)
+    torch.cuda.synchronize()
+    assert res["status"].numel() == 0
+    del pktgpu
+
+
+def test_depth_limit_and_stacks(P):
+    eth = gen.ethernet("00:00:00:00:00:01", "00:00:00:00:00:02", 0x8100).data
+    tag = gen.vlan(1, 0, 7, 0x8100).data
+    last = gen.vlan(0, 0, 5, 0x0800).data
+    ip = gen.ipv4(5, 0, 1, 64, 0, 17, "1.1.1.1", "2.2.2.2", 28).data
+    udp = gen.udp(1, 2, 8).data
+    pkts = []
+    for k in range(0, 20):
+        pkts.append(eth + tag * k + last + ip + udp)
+        pkts.append(eth + tag * k + last + ip[:-1])
+    # MPLS stacks
+    e8847 = gen.ethernet("00:00:00:00:00:01", "00:00:00:00:00:02", 0x8847).data
+    for k in range(0, 18):
+        pkts.append(e8847 + gen.mpls_raw(5, 0, 0, 9).data * k + gen.mpls_raw(6, 0, 1, 9).data +
+                    bytes([0x45, 1, 2, 3]) + ip + udp)
+    stride = 256
+    slab = np.zeros((len(pkts), stride), np.uint8)
+    lens = np.zeros(len(pkts), np.uint32)
+    for i, p in enumerate(pkts):
+        slab[i, :len(p)] = np.frombuffer(p, np.uint8)
+        lens[i] = len(p)
+    g, o = both(P, slab, len(pkts), stride=stride, lens=lens, label="stacks")
+    assert (g["status"] == schema.DEPTH_LIMIT).sum() > 5 and (g["status"] == 0).sum() > 5
+
+
+def test_gre_option_combinations(P):
+    inner = gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                  "1.1.1.1", "2.2.2.2", 0, 64, 0, 0, [], 53, 1000, False, b"x" * 8)
+    inner.remove(0)
+    pkts = []
+    for c in (0, 1):
+        for k in (0, 1):
+            for s in (0, 1):
+                p = gen.create_gre_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                          "3.3.3.3", "4.4.4.4", 0, 64, 0, 0, [], c, 0, k, s, 0, 0, 0,
+                                          0x1111, 0x2222, 0x33333333, 0x44444444, b"", inner).to_vec()
+                for L in (len(p), 38, 42, 46, 50):
+                    pkts.append(p[:L])
+    buf = b"".join(pkts)
+    lens = np.array([len(p) for p in pkts], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    both(P, np.frombuffer(buf + bytes(16), np.uint8), len(pkts), offsets=offs, lens=lens, label="gre")
+
+
+def test_fuzz_mutated_templates(P):
+    rng = np.random.default_rng(2024)
+    pkts = [p.to_vec() for p in gen.reference_22_packets()]
+    keys = [12, 13, 23, 20, 36, 37, 38, 34, 35, 16, 45, 46, 53, 57, 60, 61]
+    out = []
+    for _ in range(40000):
+        v = bytearray(pkts[int(rng.integers(0, len(pkts)))])
+        for _ in range(int(rng.integers(1, 5))):
+            k = int(rng.choice(keys)) if rng.random() < 0.6 else int(rng.integers(0, len(v)))
+            if k < len(v):
+                v[k] = int(rng.choice([0x00, 0x01, 0x04, 0x06, 0x08, 0x11, 0x29, 0x2F, 0x3A, 0x81,
+                                       0x86, 0x88, 0xAA, 0xDD, 0xBE, 0x22, 0xEB, 0x12, 0xB5, 0xF0,
+                                       int(rng.integers(0, 256))]))
+        out.append(bytes(v[:int(rng.integers(max(0, len(v) - 60), len(v) + 1))]))
+    buf = b"".join(out)
+    lens = np.array([len(p) for p in out], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    g, _ = both(P, np.frombuffer(buf + bytes(16), np.uint8), len(out), offsets=offs, lens=lens,
+                label="fuzz")
+    # spot-check against the independent Python walk too
+    for i in range(0, len(out), 997):
+        st, hdrs, po, pl = pyref.parse(out[i])
+        assert schema.STATUS_NAMES[g["status"][i]] == st
+
+
+def test_misaligned_slab_view_rejected(P):
+    ds = dev(np.zeros(256, np.uint8))
+    with pytest.raises(RuntimeError):
+        P.parse(ds[1:], stride=64, n=2)
+
+
+# ------------------------------------------------------------------ getters and checksum
+def test_extract_fields_vs_oracle(P):
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    offs, lens = gen.pcap_index_py(pc)
+    buf, offs4, lens4 = gen.gen_c4(20000, seed=77)
+    slab = buf
+    g = gpu_parse(P, slab, len(offs4), offsets=offs4, lens=lens4, columns=["chain"])
+    specs = []
+    for t in range(1, len(schema.HDR_NAMES)):
+        if t == H["STP"]:
+            continue
+        for name, s, e in oracle.field_table(t):
+            specs.append((t, 0, s, e))
+    specs += [(H["IPv4"], 1, 96, 127), (H["Ether"], 1, 0, 47), (H["IPv6"], 0, 0, 71),
+              (H["IPv6"], 1, 64, 191), (H["ARP"], 0, 3, 66)]
+    import pktgpu  # noqa: F401
+    vals, found = P.extract_fields(dev(slab), {k: dev(g[k]) for k in ("n_hdrs", "hdr_type", "hdr_off")},
+                                   specs, offsets=dev(offs4), lens=dev(lens4))
+    torch.cuda.synchronize()
+    ov, of = oracle.extract_fields(slab, len(offs4), g, specs, offsets=offs4, lens=lens4)
+    for k, sp in enumerate(specs):
+        assert np.array_equal(vals[k].cpu().numpy(), ov[k]), sp
+        assert np.array_equal(found[k].cpu().numpy(), of[k]), sp
+    del pc, offs, lens
+
+
+def test_ipv4_checksum_batch_sweep(P):
+    """tests/lib.rs:151-204 on the device: 25 400 builder headers -> Packet::ipv4_checksum."""
+    payload = bytes(range(100))
+    ips = [f"{k}.{k}.{k}.1" for k in range(10, 20)]
+    hdrs = []
+    for sip in ips:
+        for dip in ips:
+            for ttl in range(1, 255):
+                hdrs.append(gen.ipv4(5, 0, 115, ttl, 0, 6, sip, dip, 140).data)
+    a = np.frombuffer(b"".join(hdrs), np.uint8)
+    out = P.ipv4_checksum(dev(a), stride=20).cpu().numpy()
+    stored = np.array([int.from_bytes(h[10:12], "big") for h in hdrs])
+    assert np.array_equal(out, stored)
+    rng = np.random.default_rng(3)
+    r = rng.integers(0, 256, (50000, 24), dtype=np.uint8)
+    out = P.ipv4_checksum(dev(r), stride=24).cpu().numpy()
+    want = np.array([oracle.ipv4_checksum(r[i, :20].tobytes()) for i in range(0, 50000, 50)])
+    assert np.array_equal(out[::50], want)
