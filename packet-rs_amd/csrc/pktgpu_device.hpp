@@ -270,7 +270,7 @@ __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool 
                 state = S_ETHER;
                 break;
             }
-            case S_ARP: case S_ICMP: case S_TCP: next = S_ACCEPT; break;
+            case S_SNAP: case S_ARP: case S_ICMP: case S_TCP: next = S_ACCEPT; break;
             case S_UDP: next = (pv.be16(o + 2) == 4789u) ? S_VXLAN : S_ACCEPT; break;  // types.rs:7
             default: next = S_ETHER; break;  // S_VXLAN
         }
