@@ -25,178 +25,206 @@ struct pkt_ctx {
 
 namespace {
 
+// Output column groups.  A kernel is specialised on GM = the groups whose columns are ALL
+// requested (no per-column checks at all), or GM = G_RUNTIME (each column checked for NULL).
+enum : uint32_t {
+    G_CHAIN = 1, G_ETHER = 2, G_VLAN = 4, G_IPV4 = 8, G_IPV6 = 16, G_TCP = 32, G_UDP = 64,
+    G_ALL = 127, G_RUNTIME = 128
+};
+
+template <uint32_t GM, uint32_t G>
+__device__ __forceinline__ bool want(const void* p) {
+    if constexpr ((GM & G_RUNTIME) != 0) return p != nullptr;
+    else return (GM & G) != 0;
+}
+
+// Store at a 32-bit byte offset from a column base (global_store ... saddr: one VGPR offset).
+template <class T>
+__device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
+    *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff) = v;
+}
+
 // Fields of the first header of each group (Q11), from the walk's first offsets.
-__device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint64_t i, const PacketView& pv,
+// `i` is the packet index within this launch (< 2^28, so every byte offset fits 32 bits).
+template <uint32_t GM>
+__device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, const PacketView& pv,
                                             const WalkResult& r, bool ok) {
+    const uint32_t o1 = i, o2 = i * 2u, o4 = i * 4u, o8 = i * 8u, o16 = i * 16u;
     // Ether (headers.rs:530-540): dst 0-47, src 48-95, etype 96-111
-    if (out.eth_dst || out.eth_src || out.eth_etype) {
+    if (want<GM, G_ETHER>(out.eth_dst) || want<GM, G_ETHER>(out.eth_src) || want<GM, G_ETHER>(out.eth_etype)) {
         uint32_t d[4] = {0, 0, 0, 0};
-        bool h = ok && r.f_eth >= 0;
+        const bool h = ok && r.f_eth >= 0;
         if (h) pv.hdr<4>((uint32_t)r.f_eth, 14, d);
-        if (out.eth_dst) out.eth_dst[i] = h ? (((uint64_t)d[0] << 16) | (d[1] >> 16)) : 0ull;
-        if (out.eth_src) out.eth_src[i] = h ? (((uint64_t)(d[1] & 0xFFFFu) << 32) | d[2]) : 0ull;
-        if (out.eth_etype) out.eth_etype[i] = h ? (uint16_t)(d[3] >> 16) : (uint16_t)0;
+        if (want<GM, G_ETHER>(out.eth_dst)) st<uint64_t>(out.eth_dst, o8, ((uint64_t)d[0] << 16) | (d[1] >> 16));
+        if (want<GM, G_ETHER>(out.eth_src)) st<uint64_t>(out.eth_src, o8, ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[2]);
+        if (want<GM, G_ETHER>(out.eth_etype)) st<uint16_t>(out.eth_etype, o2, (uint16_t)(d[3] >> 16));
     }
     // Vlan (headers.rs:543-552): pcp 0-2, cfi 3, vid 4-15, etype 16-31
-    if (out.vlan_pcp || out.vlan_cfi || out.vlan_vid || out.vlan_etype) {
+    if (want<GM, G_VLAN>(out.vlan_pcp) || want<GM, G_VLAN>(out.vlan_cfi) || want<GM, G_VLAN>(out.vlan_vid) ||
+        want<GM, G_VLAN>(out.vlan_etype)) {
         uint32_t d[1] = {0};
-        bool h = ok && r.f_vlan >= 0;
-        if (h) pv.hdr<1>((uint32_t)r.f_vlan, 4, d);
-        if (out.vlan_pcp) out.vlan_pcp[i] = (uint8_t)(d[0] >> 29);
-        if (out.vlan_cfi) out.vlan_cfi[i] = (uint8_t)((d[0] >> 28) & 1u);
-        if (out.vlan_vid) out.vlan_vid[i] = (uint16_t)((d[0] >> 16) & 0xFFFu);
-        if (out.vlan_etype) out.vlan_etype[i] = (uint16_t)(d[0] & 0xFFFFu);
+        if (ok && r.f_vlan >= 0) pv.hdr<1>((uint32_t)r.f_vlan, 4, d);
+        if (want<GM, G_VLAN>(out.vlan_pcp)) st<uint8_t>(out.vlan_pcp, o1, (uint8_t)(d[0] >> 29));
+        if (want<GM, G_VLAN>(out.vlan_cfi)) st<uint8_t>(out.vlan_cfi, o1, (uint8_t)((d[0] >> 28) & 1u));
+        if (want<GM, G_VLAN>(out.vlan_vid)) st<uint16_t>(out.vlan_vid, o2, (uint16_t)((d[0] >> 16) & 0xFFFu));
+        if (want<GM, G_VLAN>(out.vlan_etype)) st<uint16_t>(out.vlan_etype, o2, (uint16_t)(d[0] & 0xFFFFu));
     }
     // IPv4 (headers.rs:555-574) + Packet::ipv4_checksum (packet.rs:93-107)
-    if (out.ipv4_version || out.ipv4_ihl || out.ipv4_diffserv || out.ipv4_total_len ||
-        out.ipv4_identification || out.ipv4_flags || out.ipv4_frag_startset || out.ipv4_ttl ||
-        out.ipv4_protocol || out.ipv4_header_checksum || out.ipv4_src || out.ipv4_dst ||
-        out.ipv4_csum_calc) {
+    if (want<GM, G_IPV4>(out.ipv4_version) || want<GM, G_IPV4>(out.ipv4_ihl) || want<GM, G_IPV4>(out.ipv4_diffserv) ||
+        want<GM, G_IPV4>(out.ipv4_total_len) || want<GM, G_IPV4>(out.ipv4_identification) ||
+        want<GM, G_IPV4>(out.ipv4_flags) || want<GM, G_IPV4>(out.ipv4_frag_startset) || want<GM, G_IPV4>(out.ipv4_ttl) ||
+        want<GM, G_IPV4>(out.ipv4_protocol) || want<GM, G_IPV4>(out.ipv4_header_checksum) ||
+        want<GM, G_IPV4>(out.ipv4_src) || want<GM, G_IPV4>(out.ipv4_dst) || want<GM, G_IPV4>(out.ipv4_csum_calc)) {
         uint32_t d[5] = {0, 0, 0, 0, 0};
-        bool h = ok && r.f_ipv4 >= 0;
+        const bool h = ok && r.f_ipv4 >= 0;
         if (h) pv.hdr<5>((uint32_t)r.f_ipv4, 20, d);
-        if (out.ipv4_version) out.ipv4_version[i] = (uint8_t)(d[0] >> 28);
-        if (out.ipv4_ihl) out.ipv4_ihl[i] = (uint8_t)((d[0] >> 24) & 0xFu);
-        if (out.ipv4_diffserv) out.ipv4_diffserv[i] = (uint8_t)((d[0] >> 16) & 0xFFu);
-        if (out.ipv4_total_len) out.ipv4_total_len[i] = (uint16_t)(d[0] & 0xFFFFu);
-        if (out.ipv4_identification) out.ipv4_identification[i] = (uint16_t)(d[1] >> 16);
-        if (out.ipv4_flags) out.ipv4_flags[i] = (uint8_t)((d[1] >> 13) & 7u);
-        if (out.ipv4_frag_startset) out.ipv4_frag_startset[i] = (uint16_t)(d[1] & 0x1FFFu);
-        if (out.ipv4_ttl) out.ipv4_ttl[i] = (uint8_t)(d[2] >> 24);
-        if (out.ipv4_protocol) out.ipv4_protocol[i] = (uint8_t)((d[2] >> 16) & 0xFFu);
-        if (out.ipv4_header_checksum) out.ipv4_header_checksum[i] = (uint16_t)(d[2] & 0xFFFFu);
-        if (out.ipv4_src) out.ipv4_src[i] = d[3];
-        if (out.ipv4_dst) out.ipv4_dst[i] = d[4];
-        if (out.ipv4_csum_calc) {
+        if (want<GM, G_IPV4>(out.ipv4_version)) st<uint8_t>(out.ipv4_version, o1, (uint8_t)(d[0] >> 28));
+        if (want<GM, G_IPV4>(out.ipv4_ihl)) st<uint8_t>(out.ipv4_ihl, o1, (uint8_t)((d[0] >> 24) & 0xFu));
+        if (want<GM, G_IPV4>(out.ipv4_diffserv)) st<uint8_t>(out.ipv4_diffserv, o1, (uint8_t)((d[0] >> 16) & 0xFFu));
+        if (want<GM, G_IPV4>(out.ipv4_total_len)) st<uint16_t>(out.ipv4_total_len, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_IPV4>(out.ipv4_identification)) st<uint16_t>(out.ipv4_identification, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_IPV4>(out.ipv4_flags)) st<uint8_t>(out.ipv4_flags, o1, (uint8_t)((d[1] >> 13) & 7u));
+        if (want<GM, G_IPV4>(out.ipv4_frag_startset)) st<uint16_t>(out.ipv4_frag_startset, o2, (uint16_t)(d[1] & 0x1FFFu));
+        if (want<GM, G_IPV4>(out.ipv4_ttl)) st<uint8_t>(out.ipv4_ttl, o1, (uint8_t)(d[2] >> 24));
+        if (want<GM, G_IPV4>(out.ipv4_protocol)) st<uint8_t>(out.ipv4_protocol, o1, (uint8_t)((d[2] >> 16) & 0xFFu));
+        if (want<GM, G_IPV4>(out.ipv4_header_checksum)) st<uint16_t>(out.ipv4_header_checksum, o2, (uint16_t)(d[2] & 0xFFFFu));
+        if (want<GM, G_IPV4>(out.ipv4_src)) st<uint32_t>(out.ipv4_src, o4, d[3]);
+        if (want<GM, G_IPV4>(out.ipv4_dst)) st<uint32_t>(out.ipv4_dst, o4, d[4]);
+        if (want<GM, G_IPV4>(out.ipv4_csum_calc)) {
             // nine BE words, word 5 (byte offset 10) skipped; fold ((s>>16)+s)&0xFFFF (Q1)
             uint32_t s = (d[0] >> 16) + (d[0] & 0xFFFFu) + (d[1] >> 16) + (d[1] & 0xFFFFu) +
-                         (d[2] >> 16) + (d[3] >> 16) + (d[3] & 0xFFFFu) + (d[4] >> 16) +
-                         (d[4] & 0xFFFFu);
+                         (d[2] >> 16) + (d[3] >> 16) + (d[3] & 0xFFFFu) + (d[4] >> 16) + (d[4] & 0xFFFFu);
             s = ((s >> 16) + s) & 0xFFFFu;
-            out.ipv4_csum_calc[i] = h ? (uint16_t)(~s) : (uint16_t)0;
+            st<uint16_t>(out.ipv4_csum_calc, o2, h ? (uint16_t)(~s) : (uint16_t)0);
         }
     }
     // IPv6 (headers.rs:577-592); src/dst as the raw 16 bytes of bytes(msb, lsb)
-    if (out.ipv6_version || out.ipv6_traffic_class || out.ipv6_flow_label || out.ipv6_payload_len ||
-        out.ipv6_next_hdr || out.ipv6_hop_limit || out.ipv6_src || out.ipv6_dst) {
+    if (want<GM, G_IPV6>(out.ipv6_version) || want<GM, G_IPV6>(out.ipv6_traffic_class) ||
+        want<GM, G_IPV6>(out.ipv6_flow_label) || want<GM, G_IPV6>(out.ipv6_payload_len) ||
+        want<GM, G_IPV6>(out.ipv6_next_hdr) || want<GM, G_IPV6>(out.ipv6_hop_limit) ||
+        want<GM, G_IPV6>(out.ipv6_src) || want<GM, G_IPV6>(out.ipv6_dst)) {
         uint32_t d[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        bool h = ok && r.f_ipv6 >= 0;
-        if (h) pv.hdr<10>((uint32_t)r.f_ipv6, 40, d);
-        if (out.ipv6_version) out.ipv6_version[i] = (uint8_t)(d[0] >> 28);
-        if (out.ipv6_traffic_class) out.ipv6_traffic_class[i] = (uint8_t)((d[0] >> 20) & 0xFFu);
-        if (out.ipv6_flow_label) out.ipv6_flow_label[i] = d[0] & 0xFFFFFu;
-        if (out.ipv6_payload_len) out.ipv6_payload_len[i] = (uint16_t)(d[1] >> 16);
-        if (out.ipv6_next_hdr) out.ipv6_next_hdr[i] = (uint8_t)((d[1] >> 8) & 0xFFu);
-        if (out.ipv6_hop_limit) out.ipv6_hop_limit[i] = (uint8_t)(d[1] & 0xFFu);
-        if (out.ipv6_src)
-            *reinterpret_cast<uint4*>(out.ipv6_src + 16 * i) =
-                make_uint4(bswap32(d[2]), bswap32(d[3]), bswap32(d[4]), bswap32(d[5]));
-        if (out.ipv6_dst)
-            *reinterpret_cast<uint4*>(out.ipv6_dst + 16 * i) =
-                make_uint4(bswap32(d[6]), bswap32(d[7]), bswap32(d[8]), bswap32(d[9]));
+        if (ok && r.f_ipv6 >= 0) pv.hdr<10>((uint32_t)r.f_ipv6, 40, d);
+        if (want<GM, G_IPV6>(out.ipv6_version)) st<uint8_t>(out.ipv6_version, o1, (uint8_t)(d[0] >> 28));
+        if (want<GM, G_IPV6>(out.ipv6_traffic_class)) st<uint8_t>(out.ipv6_traffic_class, o1, (uint8_t)((d[0] >> 20) & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_flow_label)) st<uint32_t>(out.ipv6_flow_label, o4, d[0] & 0xFFFFFu);
+        if (want<GM, G_IPV6>(out.ipv6_payload_len)) st<uint16_t>(out.ipv6_payload_len, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_IPV6>(out.ipv6_next_hdr)) st<uint8_t>(out.ipv6_next_hdr, o1, (uint8_t)((d[1] >> 8) & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_hop_limit)) st<uint8_t>(out.ipv6_hop_limit, o1, (uint8_t)(d[1] & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_src))
+            st<uint4>(reinterpret_cast<uint4*>(out.ipv6_src), o16,
+                      make_uint4(bswap32(d[2]), bswap32(d[3]), bswap32(d[4]), bswap32(d[5])));
+        if (want<GM, G_IPV6>(out.ipv6_dst))
+            st<uint4>(reinterpret_cast<uint4*>(out.ipv6_dst), o16,
+                      make_uint4(bswap32(d[6]), bswap32(d[7]), bswap32(d[8]), bswap32(d[9])));
     }
     // TCP (headers.rs:606-622)
-    if (out.tcp_src || out.tcp_dst || out.tcp_seq_no || out.tcp_ack_no || out.tcp_data_startset ||
-        out.tcp_res || out.tcp_flags || out.tcp_window || out.tcp_checksum || out.tcp_urgent_ptr) {
+    if (want<GM, G_TCP>(out.tcp_src) || want<GM, G_TCP>(out.tcp_dst) || want<GM, G_TCP>(out.tcp_seq_no) ||
+        want<GM, G_TCP>(out.tcp_ack_no) || want<GM, G_TCP>(out.tcp_data_startset) || want<GM, G_TCP>(out.tcp_res) ||
+        want<GM, G_TCP>(out.tcp_flags) || want<GM, G_TCP>(out.tcp_window) || want<GM, G_TCP>(out.tcp_checksum) ||
+        want<GM, G_TCP>(out.tcp_urgent_ptr)) {
         uint32_t d[5] = {0, 0, 0, 0, 0};
-        bool h = ok && r.f_tcp >= 0;
-        if (h) pv.hdr<5>((uint32_t)r.f_tcp, 20, d);
-        if (out.tcp_src) out.tcp_src[i] = (uint16_t)(d[0] >> 16);
-        if (out.tcp_dst) out.tcp_dst[i] = (uint16_t)(d[0] & 0xFFFFu);
-        if (out.tcp_seq_no) out.tcp_seq_no[i] = d[1];
-        if (out.tcp_ack_no) out.tcp_ack_no[i] = d[2];
-        if (out.tcp_data_startset) out.tcp_data_startset[i] = (uint8_t)(d[3] >> 28);
-        if (out.tcp_res) out.tcp_res[i] = (uint8_t)((d[3] >> 24) & 0xFu);
-        if (out.tcp_flags) out.tcp_flags[i] = (uint8_t)((d[3] >> 16) & 0xFFu);
-        if (out.tcp_window) out.tcp_window[i] = (uint16_t)(d[3] & 0xFFFFu);
-        if (out.tcp_checksum) out.tcp_checksum[i] = (uint16_t)(d[4] >> 16);
-        if (out.tcp_urgent_ptr) out.tcp_urgent_ptr[i] = (uint16_t)(d[4] & 0xFFFFu);
+        if (ok && r.f_tcp >= 0) pv.hdr<5>((uint32_t)r.f_tcp, 20, d);
+        if (want<GM, G_TCP>(out.tcp_src)) st<uint16_t>(out.tcp_src, o2, (uint16_t)(d[0] >> 16));
+        if (want<GM, G_TCP>(out.tcp_dst)) st<uint16_t>(out.tcp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_TCP>(out.tcp_seq_no)) st<uint32_t>(out.tcp_seq_no, o4, d[1]);
+        if (want<GM, G_TCP>(out.tcp_ack_no)) st<uint32_t>(out.tcp_ack_no, o4, d[2]);
+        if (want<GM, G_TCP>(out.tcp_data_startset)) st<uint8_t>(out.tcp_data_startset, o1, (uint8_t)(d[3] >> 28));
+        if (want<GM, G_TCP>(out.tcp_res)) st<uint8_t>(out.tcp_res, o1, (uint8_t)((d[3] >> 24) & 0xFu));
+        if (want<GM, G_TCP>(out.tcp_flags)) st<uint8_t>(out.tcp_flags, o1, (uint8_t)((d[3] >> 16) & 0xFFu));
+        if (want<GM, G_TCP>(out.tcp_window)) st<uint16_t>(out.tcp_window, o2, (uint16_t)(d[3] & 0xFFFFu));
+        if (want<GM, G_TCP>(out.tcp_checksum)) st<uint16_t>(out.tcp_checksum, o2, (uint16_t)(d[4] >> 16));
+        if (want<GM, G_TCP>(out.tcp_urgent_ptr)) st<uint16_t>(out.tcp_urgent_ptr, o2, (uint16_t)(d[4] & 0xFFFFu));
     }
     // UDP (headers.rs:625-634)
-    if (out.udp_src || out.udp_dst || out.udp_length || out.udp_checksum) {
+    if (want<GM, G_UDP>(out.udp_src) || want<GM, G_UDP>(out.udp_dst) || want<GM, G_UDP>(out.udp_length) ||
+        want<GM, G_UDP>(out.udp_checksum)) {
         uint32_t d[2] = {0, 0};
-        bool h = ok && r.f_udp >= 0;
-        if (h) pv.hdr<2>((uint32_t)r.f_udp, 8, d);
-        if (out.udp_src) out.udp_src[i] = (uint16_t)(d[0] >> 16);
-        if (out.udp_dst) out.udp_dst[i] = (uint16_t)(d[0] & 0xFFFFu);
-        if (out.udp_length) out.udp_length[i] = (uint16_t)(d[1] >> 16);
-        if (out.udp_checksum) out.udp_checksum[i] = (uint16_t)(d[1] & 0xFFFFu);
+        if (ok && r.f_udp >= 0) pv.hdr<2>((uint32_t)r.f_udp, 8, d);
+        if (want<GM, G_UDP>(out.udp_src)) st<uint16_t>(out.udp_src, o2, (uint16_t)(d[0] >> 16));
+        if (want<GM, G_UDP>(out.udp_dst)) st<uint16_t>(out.udp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_UDP>(out.udp_length)) st<uint16_t>(out.udp_length, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_UDP>(out.udp_checksum)) st<uint16_t>(out.udp_checksum, o2, (uint16_t)(d[1] & 0xFFFFu));
     }
 }
 
 // Packet i's start (byte offset in the slab) and length, clamped to the slab so that no read
 // can leave the caller's allocation whatever the batch description says.
-__device__ __forceinline__ void packet_range(const KParams& p, uint64_t i, uint64_t& off,
+__device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint64_t& off,
                                              uint32_t& len) {
     if (p.offsets) {
         off = p.offsets[i];
         len = p.lens[i];
     } else {
-        off = i * (uint64_t)p.stride;
-        len = p.lens ? p.lens[i] : p.stride;
+        off = (p.i0 + i) * (uint64_t)p.stride;
+        if (p.lens) len = p.lens[i];
+        else len = p.stride;
     }
     uint64_t room = off < p.slab_len ? p.slab_len - off : 0;
     if ((uint64_t)len > room) len = (uint32_t)room;
     if (len > 0xFFFFu) len = 0xFFFFu;  // u16 offsets/lengths in the ABI
 }
 
-template <int NCH>
+template <int NCH, uint32_t GM>
 __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
     // (NCH + 1) chunk rows per wave: the extra row is slack so a window read of dword k+1 never
     // leaves this wave's region.
     __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][(NCH + 1) * kChunkRow];
     const int lane = threadIdx.x & (kWave - 1);
     const int wv = threadIdx.x / kWave;
-    const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t i = blockIdx.x * (uint32_t)kBlock + threadIdx.x;  // within this launch
     const bool active = i < p.n;
 
     uint64_t off = 0;
     uint32_t len = 0;
     if (active) packet_range(p, i, off, len);
 
-    // ---- stage the first NCH*16 bytes (from the 16-byte-aligned start) of each packet
-    const uint64_t gaddr = (uint64_t)(uintptr_t)p.slab + off;
-    const uint64_t a0 = gaddr & ~(uint64_t)15;
-    const uint32_t shift = (uint32_t)(gaddr - a0);
-    const uint64_t slab_lo = (uint64_t)(uintptr_t)p.slab;
-    const uint64_t slab_hi16 = (slab_lo + p.slab_len + 15) & ~(uint64_t)15;  // readable end
+    // ---- stage the first NCH*16 bytes (from the 16-byte-aligned start) of each packet.
+    // Per-lane dwordx4 loads of the packet's chunks (measured faster than the LDS-DMA gather
+    // for per-packet strides: scripts/probe.py), then conflict-free ds_write_b128 into the
+    // chunk-major window (lane l of row c at c*1024 + l*16: 8-lane write groups span all banks).
+    // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
+    // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
+    const uint64_t a0 = off & ~(uint64_t)15;
+    const uint32_t shift = (uint32_t)(off - a0);
+    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
     uint8_t* win = &lds[wv][0];
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 chunk[NCH];
 #pragma unroll
     for (int c = 0; c < NCH; c++) {
-        uint64_t src = a0 + 16u * (uint32_t)c;
-        if (src + 16 > slab_hi16) src = slab_hi16 - 16;  // beyond the slab: any in-bounds chunk
-        if (src < slab_lo) src = slab_lo;
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src),
-                                         (__attribute__((address_space(3))) void*)(win + c * kChunkRow),
-                                         16, 0, 0);
+        uint64_t o = a0 + 16u * (uint32_t)c;
+        o = o > last16 ? last16 : o;
+        chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(win + c * kChunkRow + lane * 16) = chunk[c];
+    __builtin_amdgcn_wave_barrier();
 
     PacketView pv;
     pv.lw = win + lane * 16;
     pv.gbase = p.slab + off;
     pv.shift = shift;
-    uint32_t wend = (uint32_t)NCH * 16u - shift;
-    pv.win_end = wend;
+    pv.win_end = (uint32_t)NCH * 16u - shift;
     pv.len = len;
 
     const pkt_out_t& out = p.out;
-    const uint64_t n = p.n;
+    const uint64_t ns = p.n_slot_stride;
     auto push = [&](uint32_t slot, uint32_t t, uint32_t o) {
-        if (out.hdr_type) out.hdr_type[(uint64_t)slot * n + i] = (uint8_t)t;
-        if (out.hdr_off) out.hdr_off[(uint64_t)slot * n + i] = (uint16_t)o;
+        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)t;
+        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
     };
     WalkResult r;
     walk(pv, entry_state(p.entry), active, push, r);
     if (!active) return;
 
     const bool ok = r.status == PKT_OK;
-    if (out.status) out.status[i] = (uint8_t)r.status;
-    if (out.n_hdrs) out.n_hdrs[i] = ok ? (uint8_t)r.n : (uint8_t)0;
-    if (out.payload_off) out.payload_off[i] = ok ? (uint16_t)r.payload_off : (uint16_t)0;
-    if (out.payload_len) out.payload_len[i] = ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0;
-    if (out.hdr_mask) out.hdr_mask[i] = ok ? r.mask : 0u;
-    emit_fields(out, i, pv, r, ok);
+    if (want<GM, G_CHAIN>(out.status)) st<uint8_t>(out.status, i, (uint8_t)r.status);
+    if (want<GM, G_CHAIN>(out.n_hdrs)) st<uint8_t>(out.n_hdrs, i, ok ? (uint8_t)r.n : (uint8_t)0);
+    if (want<GM, G_CHAIN>(out.payload_off)) st<uint16_t>(out.payload_off, 2 * i, ok ? (uint16_t)r.payload_off : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.payload_len)) st<uint16_t>(out.payload_len, 2 * i, ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.hdr_mask)) st<uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
+    emit_fields<GM>(out, i, pv, r, ok);
 }
 
 // Batched `<Hdr>Slice::<field>()` (headers.rs:195-201 -> bit_range 252-263).
@@ -277,12 +305,47 @@ int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
     return PKT_ERR_HIP;
 }
 
-template <int NCH>
+template <int NCH, uint32_t GM>
 hipError_t launch_parse(const KParams& kp, hipStream_t s) {
     dim3 grid((unsigned)((kp.n + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL(parse_kernel<NCH>, grid, dim3(kBlock), 0, s, kp);
+    hipLaunchKernelGGL((parse_kernel<NCH, GM>), grid, dim3(kBlock), 0, s, kp);
     return hipGetLastError();
 }
+
+template <int NCH>
+hipError_t launch_gm(const KParams& kp, uint32_t gm, hipStream_t s) {
+    switch (gm) {
+        case G_CHAIN: return launch_parse<NCH, G_CHAIN>(kp, s);
+        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_parse<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP>(kp, s);
+        case G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP:
+            return launch_parse<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP>(kp, s);
+        case G_ALL: return launch_parse<NCH, G_ALL>(kp, s);
+        default: return launch_parse<NCH, G_RUNTIME>(kp, s);
+    }
+}
+
+// Which groups are fully requested (all columns non-NULL) and which partly.
+void group_masks(const pkt_out_t& o, uint32_t& full, uint32_t& any) {
+    const void* const* cols = reinterpret_cast<const void* const*>(&o);
+    // column ranges of each group in pkt_out_t order (see include/pktgpu.h)
+    static const struct { uint32_t g; int lo, hi; } R[] = {
+        {G_CHAIN, 0, 7}, {G_ETHER, 7, 10}, {G_VLAN, 10, 14}, {G_IPV4, 14, 27},
+        {G_IPV6, 27, 35}, {G_TCP, 35, 45}, {G_UDP, 45, 49}};
+    static_assert(sizeof(pkt_out_t) == 49 * sizeof(void*), "pkt_out_t layout");
+    full = any = 0;
+    for (const auto& g : R) {
+        bool all = true, some = false;
+        for (int c = g.lo; c < g.hi; c++) {
+            all &= cols[c] != nullptr;
+            some |= cols[c] != nullptr;
+        }
+        if (all) full |= g.g;
+        if (some) any |= g.g;
+    }
+}
+
+template <class T>
+T* adv(T* p, uint64_t k) { return p ? p + k : p; }
 
 }  // namespace
 
@@ -337,23 +400,39 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);
 
-    KParams kp;
-    kp.slab = b->slab;
-    kp.slab_len = b->slab_len;
-    kp.offsets = b->offsets;
-    kp.lens = b->lens;
-    kp.stride = b->stride;
-    kp.entry = entry;
-    kp.n = b->n;
-    kp.out = *out;
+    uint32_t full, any;
+    group_masks(*out, full, any);
+    const uint32_t gm = (full == any) ? full : G_RUNTIME;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (nch <= 2) e = launch_parse<2>(kp, s);
-    else if (nch <= 4) e = launch_parse<4>(kp, s);
-    else if (nch <= 5) e = launch_parse<5>(kp, s);
-    else if (nch <= 8) e = launch_parse<8>(kp, s);
-    else if (nch <= 9) e = launch_parse<9>(kp, s);
-    else if (nch <= 16) e = launch_parse<16>(kp, s);
-    else e = launch_parse<17>(kp, s);
+    const uint64_t kChunk = 1ull << 26;  // packets per launch (32-bit byte offsets in-kernel)
+    for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kChunk) {
+        const uint64_t cnt = std::min<uint64_t>(kChunk, b->n - i0);
+        KParams kp;
+        kp.slab = b->slab;
+        kp.slab_len = b->slab_len;
+        kp.offsets = adv(b->offsets, i0);
+        kp.lens = adv(b->lens, i0);
+        kp.i0 = i0;
+        kp.n_slot_stride = b->n;
+        kp.stride = b->stride;
+        kp.n = (uint32_t)cnt;
+        kp.entry = entry;
+        pkt_out_t o = *out;
+        uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
+        static const uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
+                                          1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
+                                          1, 1, 2, 2, 2, 2, 2, 2, 2};
+        for (int c = 0; c < 49; c++)
+            if (oc[c]) oc[c] += i0 * kSize[c];
+        kp.out = o;
+        if (nch <= 2) e = launch_gm<2>(kp, gm, s);
+        else if (nch <= 4) e = launch_gm<4>(kp, gm, s);
+        else if (nch <= 5) e = launch_gm<5>(kp, gm, s);
+        else if (nch <= 8) e = launch_gm<8>(kp, gm, s);
+        else if (nch <= 9) e = launch_gm<9>(kp, gm, s);
+        else if (nch <= 16) e = launch_gm<16>(kp, gm, s);
+        else e = launch_gm<17>(kp, gm, s);
+    }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;
 }

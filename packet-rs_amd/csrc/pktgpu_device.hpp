@@ -37,14 +37,19 @@ enum State : uint32_t {
 // pkt_entry_t -> first state (entries 1..17 map 1:1 onto S_DOT3..S_VXLAN)
 __device__ __forceinline__ uint32_t entry_state(int entry) { return (uint32_t)entry; }
 
+// One launch covers packets [i0, i0 + n) of a batch (n < 2^28 so that every per-packet byte
+// offset fits 32 bits); offsets/lens/per-packet columns are pre-offset by i0 on the host, the
+// slot-major hdr_type/hdr_off columns are pre-offset by i0 and strided by the batch size.
 struct KParams {
     const uint8_t* slab;
     uint64_t slab_len;
     const uint64_t* offsets;
     const uint32_t* lens;
+    uint64_t i0;
+    uint64_t n_slot_stride;
     uint32_t stride;
+    uint32_t n;
     int entry;
-    uint64_t n;
     pkt_out_t out;
 };
 
@@ -141,145 +146,179 @@ struct WalkResult {
     int32_t f_eth, f_vlan, f_ipv4, f_ipv6, f_tcp, f_udp;  // first offsets, -1 = absent
 };
 
-// The walk.  `push` records (type, offset) in list slot `n`.
+// Header type and size recorded by the walk state S (make_header! sizes, headers.rs:529-827).
+template <uint32_t S> struct StateHdr;
+template <> struct StateHdr<S_DOT3> { static constexpr uint32_t T = PKT_HDR_DOT3, SZ = 14; };
+template <> struct StateHdr<S_LLC> { static constexpr uint32_t T = PKT_HDR_LLC, SZ = 3; };
+template <> struct StateHdr<S_SNAP> { static constexpr uint32_t T = PKT_HDR_SNAP, SZ = 5; };
+template <> struct StateHdr<S_ETHER> { static constexpr uint32_t T = PKT_HDR_ETHER, SZ = 14; };
+template <> struct StateHdr<S_VLAN> { static constexpr uint32_t T = PKT_HDR_VLAN, SZ = 4; };
+template <> struct StateHdr<S_MPLS> { static constexpr uint32_t T = PKT_HDR_MPLS, SZ = 4; };
+template <> struct StateHdr<S_MPLS_BOS> { static constexpr uint32_t T = PKT_HDR_MPLS, SZ = 4; };
+template <> struct StateHdr<S_IPV4> { static constexpr uint32_t T = PKT_HDR_IPV4, SZ = 20; };
+template <> struct StateHdr<S_IPV6> { static constexpr uint32_t T = PKT_HDR_IPV6, SZ = 40; };
+template <> struct StateHdr<S_GRE> { static constexpr uint32_t T = PKT_HDR_GRE, SZ = 4; };
+template <> struct StateHdr<S_ERSPAN2> { static constexpr uint32_t T = PKT_HDR_ERSPAN2, SZ = 8; };
+template <> struct StateHdr<S_ERSPAN3> { static constexpr uint32_t T = PKT_HDR_ERSPAN3, SZ = 12; };
+template <> struct StateHdr<S_ARP> { static constexpr uint32_t T = PKT_HDR_ARP, SZ = 28; };
+template <> struct StateHdr<S_ICMP> { static constexpr uint32_t T = PKT_HDR_ICMP, SZ = 4; };
+template <> struct StateHdr<S_TCP> { static constexpr uint32_t T = PKT_HDR_TCP, SZ = 20; };
+template <> struct StateHdr<S_UDP> { static constexpr uint32_t T = PKT_HDR_UDP, SZ = 8; };
+template <> struct StateHdr<S_VXLAN> { static constexpr uint32_t T = PKT_HDR_VXLAN, SZ = 8; };
+
+// Per-lane walk state.
+struct Lane {
+    uint32_t st, o, steps;
+    bool live;
+    WalkResult r;
+};
+
+// Record (type T, offset) in list slot r.n (PacketSlice::insert order, packet.rs:724-726).
+template <uint32_t T, class Push>
+__device__ __forceinline__ void rec(Lane& L, uint32_t off, Push& push) {
+    push(L.r.n, T, off);
+    L.r.n++;
+    L.r.mask |= 1u << T;
+    if constexpr (T == PKT_HDR_ETHER) { if (L.r.f_eth < 0) L.r.f_eth = (int32_t)off; }
+    if constexpr (T == PKT_HDR_VLAN) { if (L.r.f_vlan < 0) L.r.f_vlan = (int32_t)off; }
+    if constexpr (T == PKT_HDR_IPV4) { if (L.r.f_ipv4 < 0) L.r.f_ipv4 = (int32_t)off; }
+    if constexpr (T == PKT_HDR_IPV6) { if (L.r.f_ipv6 < 0) L.r.f_ipv6 = (int32_t)off; }
+    if constexpr (T == PKT_HDR_TCP) { if (L.r.f_tcp < 0) L.r.f_tcp = (int32_t)off; }
+    if constexpr (T == PKT_HDR_UDP) { if (L.r.f_udp < 0) L.r.f_udp = (int32_t)off; }
+}
+
+__device__ __forceinline__ void fail(Lane& L, uint32_t st) {
+    L.r.status = st;
+    L.live = false;
+}
+
+// One step of the walk for a lane in state S: bounds (the reference's slice panic, Q7), then
+// depth, then the dispatch field, record, advance.  fast.rs line numbers per state.
+template <uint32_t S, class Push>
+__device__ __forceinline__ void step(Lane& L, const PacketView& pv, Push& push) {
+    const uint32_t o = L.o, len = pv.len;
+    if constexpr (S == S_ACCEPT) {  // fast.rs:223-227
+        L.r.payload_off = o;
+        L.live = false;
+    } else if constexpr (S == S_PARSE) {  // fast.rs:5-12 reads arr[12], arr[13]
+        if (o + 14 > len) { fail(L, PKT_TRUNCATED); return; }
+        L.st = (pv.be16(o + 12) < 1500u) ? S_DOT3 : S_ETHER;
+    } else {
+        constexpr uint32_t T = StateHdr<S>::T, SZ = StateHdr<S>::SZ;
+        if (o + SZ > len) { fail(L, PKT_TRUNCATED); return; }     // `&arr[0..X::size()]`
+        if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+        if constexpr (S == S_GRE) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
+            const uint32_t w = bswap32(pv.le(o, 4));
+            const uint32_t c = w >> 31, k = (w >> 29) & 1u, s = (w >> 28) & 1u;
+            rec<T>(L, o, push);
+            uint32_t q = o + 4, oc = 0, okey = 0, oseq = 0;
+            if (c) {
+                if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+                if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+                oc = q; q += 4;
+            }
+            if (k) {
+                if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+                if (L.r.n + c >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+                okey = q; q += 4;
+            }
+            if (s) {
+                if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+                if (L.r.n + c + k >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+                oseq = q; q += 4;
+            }
+            if (s) rec<PKT_HDR_GRE_SEQUENCE_NUM>(L, oseq, push);
+            if (k) rec<PKT_HDR_GRE_KEY>(L, okey, push);
+            if (c) rec<PKT_HDR_GRE_CHKSUM_OFFSET>(L, oc, push);
+            L.o = q;
+            L.st = gre_next(w & 0xFFFFu);
+        } else if constexpr (S == S_ERSPAN3) {  // fast.rs:172-192: o bit (95) -> ERSPANPLATFORM
+            const uint32_t ob = pv.u8(o + 11) & 1u;
+            rec<T>(L, o, push);
+            uint32_t q = o + 12;
+            if (ob) {
+                if (q + 8 > len) { fail(L, PKT_TRUNCATED); return; }
+                if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+                rec<PKT_HDR_ERSPAN_PLATFORM>(L, q, push);
+                q += 8;
+            }
+            L.o = q;
+            L.st = S_ETHER;
+        } else {
+            uint32_t next;
+            if constexpr (S == S_DOT3) next = S_LLC;
+            else if constexpr (S == S_LLC)  // fast.rs:21: aa aa 03 -> SNAP
+                next = ((pv.le(o, 3) & 0xFFFFFFu) == 0x03AAAAu) ? S_SNAP : S_ACCEPT;
+            else if constexpr (S == S_ETHER) next = etype_next(pv.be16(o + 12));
+            else if constexpr (S == S_VLAN) next = etype_next(pv.be16(o + 2));
+            else if constexpr (S == S_MPLS) next = (pv.u8(o + 2) & 1u) ? S_MPLS_BOS : S_MPLS;  // bos bit 23
+            else if constexpr (S == S_MPLS_BOS) {  // fast.rs:74-83: arr[MPLS::size()] must exist (Q3)
+                if (o + 5 > len) { fail(L, PKT_TRUNCATED); return; }
+                const uint32_t nib = pv.u8(o + 4) >> 4;
+                next = (nib == 4u) ? S_IPV4 : ((nib == 6u) ? S_IPV6 : S_ETHER);
+            } else if constexpr (S == S_IPV4) next = ipproto_next(pv.u8(o + 9), false);
+            else if constexpr (S == S_IPV6) next = ipproto_next(pv.u8(o + 6), true);
+            else if constexpr (S == S_UDP) next = (pv.be16(o + 2) == 4789u) ? S_VXLAN : S_ACCEPT;  // types.rs:7
+            else if constexpr (S == S_SNAP || S == S_ARP || S == S_ICMP || S == S_TCP) next = S_ACCEPT;
+            else next = S_ETHER;  // ERSPAN2, VXLAN
+            rec<T>(L, o, push);
+            L.o = o + SZ;
+            L.st = next;
+        }
+    }
+}
+
+// The walk: a waterfall over the distinct states present in the wave.  Each iteration takes the
+// state of the first live lane (v_readlane), and every live lane in that state advances one
+// step under a SCALAR switch — a wave whose packets share a layout runs exactly one case per
+// header, a mixed wave one case per distinct state.
 template <class Push>
 __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool active, Push&& push,
-                                     WalkResult& r) {
-    r.status = PKT_OK;
-    r.n = 0;
-    r.payload_off = 0;
-    r.mask = 0;
-    r.f_eth = r.f_vlan = r.f_ipv4 = r.f_ipv6 = r.f_tcp = r.f_udp = -1;
-    uint32_t o = 0;
-    const uint32_t len = pv.len;
-    bool live = active;
-
-    auto rec = [&](uint32_t t, uint32_t off) {
-        push(r.n, t, off);
-        r.n++;
-        r.mask |= 1u << t;
-        if (t == PKT_HDR_ETHER && r.f_eth < 0) r.f_eth = (int32_t)off;
-        if (t == PKT_HDR_VLAN && r.f_vlan < 0) r.f_vlan = (int32_t)off;
-        if (t == PKT_HDR_IPV4 && r.f_ipv4 < 0) r.f_ipv4 = (int32_t)off;
-        if (t == PKT_HDR_IPV6 && r.f_ipv6 < 0) r.f_ipv6 = (int32_t)off;
-        if (t == PKT_HDR_TCP && r.f_tcp < 0) r.f_tcp = (int32_t)off;
-        if (t == PKT_HDR_UDP && r.f_udp < 0) r.f_udp = (int32_t)off;
-    };
-    auto fail = [&](uint32_t st) {
-        r.status = st;
-        live = false;
-    };
-
-    // Each iteration consumes >= 1 header (or resolves S_PARSE / accepts), so this bound is
-    // never the one that stops a walk; it only guarantees termination.
-    for (int it = 0; it < PKT_MAX_HDRS + 3; it++) {
-        if (!__any(live)) break;
-        if (!live) continue;
-        if (state == S_ACCEPT) {  // fast.rs:223-227
-            r.payload_off = o;
-            live = false;
-            continue;
-        }
-        if (state == S_PARSE) {  // fast.rs:5-12: arr[12], arr[13]
-            if (o + 14 > len) { fail(PKT_TRUNCATED); continue; }
-            state = (pv.be16(o + 12) < 1500u) ? S_DOT3 : S_ETHER;
-            continue;
-        }
-        // header size and type of this state
-        uint32_t sz, t;
-        switch (state) {
-            case S_DOT3: sz = 14; t = PKT_HDR_DOT3; break;
-            case S_LLC: sz = 3; t = PKT_HDR_LLC; break;
-            case S_SNAP: sz = 5; t = PKT_HDR_SNAP; break;
-            case S_ETHER: sz = 14; t = PKT_HDR_ETHER; break;
-            case S_VLAN: sz = 4; t = PKT_HDR_VLAN; break;
-            case S_MPLS: sz = 4; t = PKT_HDR_MPLS; break;
-            case S_MPLS_BOS: sz = 4; t = PKT_HDR_MPLS; break;
-            case S_IPV4: sz = 20; t = PKT_HDR_IPV4; break;
-            case S_IPV6: sz = 40; t = PKT_HDR_IPV6; break;
-            case S_GRE: sz = 4; t = PKT_HDR_GRE; break;
-            case S_ERSPAN2: sz = 8; t = PKT_HDR_ERSPAN2; break;
-            case S_ERSPAN3: sz = 12; t = PKT_HDR_ERSPAN3; break;
-            case S_ARP: sz = 28; t = PKT_HDR_ARP; break;
-            case S_ICMP: sz = 4; t = PKT_HDR_ICMP; break;
-            case S_TCP: sz = 20; t = PKT_HDR_TCP; break;
-            case S_UDP: sz = 8; t = PKT_HDR_UDP; break;
-            default: sz = 8; t = PKT_HDR_VXLAN; break;  // S_VXLAN
-        }
-        if (o + sz > len) { fail(PKT_TRUNCATED); continue; }   // `&arr[0..X::size()]`
-        if (r.n >= PKT_MAX_HDRS) { fail(PKT_DEPTH_LIMIT); continue; }
-        uint32_t next = S_ETHER;
-        bool advanced = false;  // multi-header steps (GRE, ERSPAN3) record and advance themselves
-        switch (state) {
-            case S_DOT3: next = S_LLC; break;
-            case S_LLC:  // fast.rs:21: aa aa 03 -> SNAP
-                next = ((pv.le(o, 3) & 0xFFFFFFu) == 0x03AAAAu) ? S_SNAP : S_ACCEPT;
-                break;
-            case S_ETHER: next = etype_next(pv.be16(o + 12)); break;
-            case S_VLAN: next = etype_next(pv.be16(o + 2)); break;
-            case S_MPLS: next = (pv.u8(o + 2) & 1u) ? S_MPLS_BOS : S_MPLS; break;  // bos = bit 23
-            case S_MPLS_BOS: {  // fast.rs:74-83: arr[MPLS::size()] must exist
-                if (o + 5 > len) { fail(PKT_TRUNCATED); advanced = true; break; }
-                uint32_t nib = pv.u8(o + 4) >> 4;
-                next = (nib == 4u) ? S_IPV4 : ((nib == 6u) ? S_IPV6 : S_ETHER);
-                break;
+                                     WalkResult& out) {
+    Lane L;
+    L.st = state;
+    L.o = 0;
+    L.steps = 0;
+    L.live = active;
+    L.r.status = PKT_OK;
+    L.r.n = 0;
+    L.r.payload_off = 0;
+    L.r.mask = 0;
+    L.r.f_eth = L.r.f_vlan = L.r.f_ipv4 = L.r.f_ipv6 = L.r.f_tcp = L.r.f_udp = -1;
+    for (;;) {
+        const uint64_t pend = __ballot(L.live);
+        if (pend == 0) break;
+        const uint32_t s0 = __builtin_amdgcn_readlane(L.st, (uint32_t)__builtin_ctzll(pend));
+        if (L.live && L.st == s0) {
+            // at most PKT_MAX_HDRS headers + parse + accept + the failing step
+            if (++L.steps > PKT_MAX_HDRS + 3) {
+                fail(L, PKT_DEPTH_LIMIT);
+            } else {
+                switch (s0) {
+                    case S_PARSE: step<S_PARSE>(L, pv, push); break;
+                    case S_DOT3: step<S_DOT3>(L, pv, push); break;
+                    case S_LLC: step<S_LLC>(L, pv, push); break;
+                    case S_SNAP: step<S_SNAP>(L, pv, push); break;
+                    case S_ETHER: step<S_ETHER>(L, pv, push); break;
+                    case S_VLAN: step<S_VLAN>(L, pv, push); break;
+                    case S_MPLS: step<S_MPLS>(L, pv, push); break;
+                    case S_MPLS_BOS: step<S_MPLS_BOS>(L, pv, push); break;
+                    case S_IPV4: step<S_IPV4>(L, pv, push); break;
+                    case S_IPV6: step<S_IPV6>(L, pv, push); break;
+                    case S_GRE: step<S_GRE>(L, pv, push); break;
+                    case S_ERSPAN2: step<S_ERSPAN2>(L, pv, push); break;
+                    case S_ERSPAN3: step<S_ERSPAN3>(L, pv, push); break;
+                    case S_ARP: step<S_ARP>(L, pv, push); break;
+                    case S_ICMP: step<S_ICMP>(L, pv, push); break;
+                    case S_TCP: step<S_TCP>(L, pv, push); break;
+                    case S_UDP: step<S_UDP>(L, pv, push); break;
+                    case S_VXLAN: step<S_VXLAN>(L, pv, push); break;
+                    default: step<S_ACCEPT>(L, pv, push); break;
+                }
             }
-            case S_IPV4: next = ipproto_next(pv.u8(o + 9), false); break;
-            case S_IPV6: next = ipproto_next(pv.u8(o + 6), true); break;
-            case S_GRE: {  // fast.rs:114-165; options sliced C, K, S; listed S, K, C (Q2)
-                advanced = true;
-                uint32_t w = bswap32(pv.le(o, 4));
-                uint32_t c = w >> 31, k = (w >> 29) & 1u, s = (w >> 28) & 1u;
-                rec(t, o);
-                uint32_t q = o + 4, oc = 0, okey = 0, oseq = 0;
-                if (c) {
-                    if (q + 4 > len) { fail(PKT_TRUNCATED); break; }
-                    if (r.n >= PKT_MAX_HDRS) { fail(PKT_DEPTH_LIMIT); break; }
-                    oc = q; q += 4;
-                }
-                if (k) {
-                    if (q + 4 > len) { fail(PKT_TRUNCATED); break; }
-                    if (r.n + c >= PKT_MAX_HDRS) { fail(PKT_DEPTH_LIMIT); break; }
-                    okey = q; q += 4;
-                }
-                if (s) {
-                    if (q + 4 > len) { fail(PKT_TRUNCATED); break; }
-                    if (r.n + c + k >= PKT_MAX_HDRS) { fail(PKT_DEPTH_LIMIT); break; }
-                    oseq = q; q += 4;
-                }
-                if (s) rec(PKT_HDR_GRE_SEQUENCE_NUM, oseq);
-                if (k) rec(PKT_HDR_GRE_KEY, okey);
-                if (c) rec(PKT_HDR_GRE_CHKSUM_OFFSET, oc);
-                o = q;
-                state = gre_next(w & 0xFFFFu);
-                break;
-            }
-            case S_ERSPAN2: next = S_ETHER; break;
-            case S_ERSPAN3: {  // fast.rs:172-192: o bit = bit 95 -> ERSPANPLATFORM
-                advanced = true;
-                uint32_t ob = pv.u8(o + 11) & 1u;
-                rec(t, o);
-                uint32_t q = o + 12;
-                if (ob) {
-                    if (q + 8 > len) { fail(PKT_TRUNCATED); break; }
-                    if (r.n >= PKT_MAX_HDRS) { fail(PKT_DEPTH_LIMIT); break; }
-                    rec(PKT_HDR_ERSPAN_PLATFORM, q);
-                    q += 8;
-                }
-                o = q;
-                state = S_ETHER;
-                break;
-            }
-            case S_SNAP: case S_ARP: case S_ICMP: case S_TCP: next = S_ACCEPT; break;
-            case S_UDP: next = (pv.be16(o + 2) == 4789u) ? S_VXLAN : S_ACCEPT; break;  // types.rs:7
-            default: next = S_ETHER; break;  // S_VXLAN
         }
-        if (advanced) continue;
-        rec(t, o);
-        o += sz;
-        state = next;
     }
-    if (live) r.status = PKT_DEPTH_LIMIT;  // unreachable bound (see loop comment)
+    out = L.r;
 }
 
 }  // namespace pktgpu
