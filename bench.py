@@ -38,9 +38,12 @@ def parse_args():
     ap.add_argument("--config", default="c2", choices=["c2", "c3", "c4"])
     ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU per step")
     ap.add_argument("--ring-gib", type=float, default=1.0)
-    ap.add_argument("--columns", default="chain,ether,ipv4,udp")
+    ap.add_argument("--columns", default=None,
+                    help="column groups; default per config: c2 chain,ether,ipv4,udp; "
+                         "c3 chain,ether,vlan,ipv4,tcp,udp; c4 all")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--streams", type=int, default=2,
                     help="consecutive steps are issued round-robin on this many HIP streams")
     return ap.parse_args()
@@ -99,16 +102,25 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     import torch.distributed as dist
+    ndev = torch.cuda.device_count()
+    gpu = local % max(1, ndev)  # rehearsal only: several ranks may share one device (gloo)
     if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        torch.cuda.set_device(gpu)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group(args.backend)
+    dev = torch.device("cuda", gpu)
     torch.cuda.set_device(dev)
 
     import pktgpu
     from pktgpu import schema
-    P = pktgpu.Parser(local)
-    cols = pktgpu.resolve_columns(args.columns.split(","))
+    P = pktgpu.Parser(gpu)
+    default_cols = {"c2": "chain,ether,ipv4,udp", "c3": "chain,ether,vlan,ipv4,tcp,udp",
+                    "c4": "all"}[args.config]
+    if args.columns is None:
+        args.columns = default_cols
+    cols = pktgpu.resolve_columns("all" if args.columns == "all" else args.columns.split(","))
     n = args.packets
 
     # ---------------- input: one seeded batch per rank, replicated over a >= ring_gib ring
@@ -174,7 +186,7 @@ def main():
     elapsed = time.perf_counter() - t0
     region_ms = e0.elapsed_time(e1)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if args.backend == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -194,7 +206,7 @@ def main():
     # ---------------- gather of one step's tuples to rank 0 (N > 1), timed separately
     gather = None
     if world > 1:
-        buf = outs[0][0]
+        buf = outs[0][0] if args.backend == "nccl" else outs[0][0].cpu()
         glist = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
         dist.gather(buf, glist, dst=0)  # warm
         torch.cuda.synchronize()
@@ -209,7 +221,8 @@ def main():
         gms = (time.perf_counter() - tg) / reps * 1e3
         gbytes = buf.numel() * (world - 1)
         gather = {"ms": round(gms, 4), "bytes_into_root": gbytes,
-                  "GB/s": round(gbytes / (gms * 1e-3) / 1e9, 2), "backend": "nccl(RCCL)",
+                  "GB/s": round(gbytes / (gms * 1e-3) / 1e9, 2),
+                  "backend": "nccl(RCCL)" if args.backend == "nccl" else args.backend,
                   "packets": n * world}
 
     if rank != 0:
@@ -265,7 +278,7 @@ def main():
     }
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this config, if any
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath) and args.columns == "chain,ether,ipv4,udp":
+    if os.path.exists(tpath) and args.columns == default_cols and n == 1 << 20:
         t = json.load(open(tpath))
         res["roofline"]["traffic"] = t["traffic_bytes_per_launch"]
         res["roofline"]["traffic_source"] = (f"profiles/traffic_{args.config}.json: rocprofv3 --pmc "

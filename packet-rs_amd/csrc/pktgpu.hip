@@ -203,7 +203,9 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
 
     PacketView pv;
     pv.lw = win + lane * 16;
-    pv.gbase = p.slab + off;
+    pv.slab = p.slab;
+    pv.off = off;
+    pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
     pv.shift = shift;
     pv.win_end = (uint32_t)NCH * 16u - shift;
     pv.len = len;
@@ -395,7 +397,9 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
     // Window: bytes of each packet staged in LDS.  Fixed stride: the slot (up to 128 B);
     // indexed: 128 B.  Unaligned packet starts need one more chunk.
     uint32_t w = ctx->window;
-    if (w == 0) w = b->offsets ? 128u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 128u);
+    // Auto window: 64 bytes hold every header of the common chains (Ether[/Vlan x2]/IPv4/TCP
+    // ends at byte 62); deeper chains (tunnels) read the rest through L2.
+    if (w == 0) w = b->offsets ? 64u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);

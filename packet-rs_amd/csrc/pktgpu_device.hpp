@@ -89,7 +89,9 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 // A lane's view of its packet: LDS window + global fallback.
 struct PacketView {
     const uint8_t* lw;        // LDS window base of this wave (chunk-major), already + lane*16
-    const uint8_t* gbase;     // packet start in global memory
+    const uint8_t* slab;      // slab base (16-byte aligned)
+    uint64_t off;             // packet start in the slab
+    uint64_t last4;           // last readable aligned dword offset of the slab
     uint32_t shift;           // packet start - aligned window start (0..15)
     uint32_t win_end;         // packet bytes [0, win_end) are in the window
     uint32_t len;             // packet length
@@ -98,8 +100,14 @@ struct PacketView {
     __device__ __forceinline__ uint32_t wdw(uint32_t k) const {
         return *reinterpret_cast<const uint32_t*>(lw + (k >> 2) * kChunkRow + (k & 3) * 4);
     }
+    // aligned dword of the slab containing slab byte a (clamped to the readable end)
+    __device__ __forceinline__ uint32_t gdw(uint64_t a) const {
+        uint64_t d = a & ~(uint64_t)3;
+        d = d > last4 ? last4 : d;
+        return *reinterpret_cast<const uint32_t*>(slab + d);
+    }
     // n (1..4) bytes at packet offset b, little-endian in the low bytes (garbage above n).
-    // Caller guarantees b + n <= len.
+    // Caller guarantees b + n <= len.  Bytes past the window come from global memory (L2).
     __device__ __forceinline__ uint32_t le(uint32_t b, uint32_t n) const {
         if (b + n <= win_end) {
             uint32_t wb = b + shift;
@@ -108,36 +116,36 @@ struct PacketView {
             uint32_t hi = (sh + n > 4) ? wdw(k + 1) : 0u;
             return __builtin_amdgcn_alignbyte(hi, lo, sh);
         }
-        uint32_t v = 0;
-        for (uint32_t i = 0; i < n; i++) v |= (uint32_t)gbase[b + i] << (8 * i);
-        return v;
+        const uint64_t a = off + b;
+        const uint32_t sh = (uint32_t)(a & 3);
+        const uint32_t lo = gdw(a);
+        const uint32_t hi = (sh + n > 4) ? gdw(a + 4) : 0u;
+        return __builtin_amdgcn_alignbyte(hi, lo, sh);
     }
     __device__ __forceinline__ uint32_t u8(uint32_t b) const { return le(b, 1) & 0xFFu; }
     __device__ __forceinline__ uint32_t be16(uint32_t b) const { return bswap32(le(b, 2)) >> 16; }
 
-    // NW big-endian dwords of header bytes [b, b + nbytes) (bytes beyond nbytes read as
-    // whatever follows in the window, or 0 on the global path).  Caller: b + nbytes <= len.
+    // NW big-endian dwords of header bytes [b, b + 4*NW) (bytes past the header's own
+    // `nbytes` are whatever follows and are never interpreted).  Caller: b + nbytes <= len.
     template <int NW>
     __device__ __forceinline__ void hdr(uint32_t b, uint32_t nbytes, uint32_t (&d)[NW]) const {
+        (void)nbytes;
+        uint32_t a[NW + 1];
+        uint32_t sh;
         if (b + 4 * NW <= win_end) {
-            uint32_t wb = b + shift;
-            uint32_t k = wb >> 2, sh = wb & 3;
-            uint32_t a[NW + 1];
+            const uint32_t wb = b + shift;
+            const uint32_t k = wb >> 2;
+            sh = wb & 3;
 #pragma unroll
             for (int i = 0; i <= NW; i++) a[i] = wdw(k + i);
-#pragma unroll
-            for (int i = 0; i < NW; i++) d[i] = bswap32(__builtin_amdgcn_alignbyte(a[i + 1], a[i], sh));
         } else {
+            const uint64_t ga = off + b;
+            sh = (uint32_t)(ga & 3);
 #pragma unroll
-            for (int i = 0; i < NW; i++) {
-                uint32_t v = 0;
-                for (uint32_t j = 0; j < 4; j++) {
-                    uint32_t bb = b + 4 * i + j;
-                    v = (v << 8) | ((4 * i + j < nbytes) ? (uint32_t)gbase[bb] : 0u);
-                }
-                d[i] = v;
-            }
+            for (int i = 0; i <= NW; i++) a[i] = gdw(ga + 4u * i);
         }
+#pragma unroll
+        for (int i = 0; i < NW; i++) d[i] = bswap32(__builtin_amdgcn_alignbyte(a[i + 1], a[i], sh));
     }
 };
 

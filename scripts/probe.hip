@@ -175,3 +175,16 @@ extern "C" int probe_write(int which, const uint8_t* slab, uint32_t n, void* con
     else hipLaunchKernelGGL(k_write_lds, dim3(grid), dim3(256), 0, s, slab, n, c);
     return hipGetLastError() == hipSuccess ? 0 : -2;
 }
+
+// H: read the first `rd` bytes (multiple of 16, <= 64) of each `stride`-byte slot.
+__global__ __launch_bounds__(256) void k_read_prefix(const uint8_t* slab, uint32_t n, uint32_t stride, uint32_t rd, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint4* p = (const uint4*)(slab + (uint64_t)min(i, n - 1) * stride);
+    uint32_t h = 0;
+    for (uint32_t c = 0; c < rd / 16; c++) h ^= mix(p[c]) + c;
+    if (i < n) out[i] = h;
+}
+extern "C" int probe_prefix(const uint8_t* slab, uint32_t n, uint32_t stride, uint32_t rd, uint32_t* out, void* stream) {
+    hipLaunchKernelGGL(k_read_prefix, dim3((n + 255) / 256), dim3(256), 0, (hipStream_t)stream, slab, n, stride, rd, out);
+    return hipGetLastError() == hipSuccess ? 0 : -2;
+}
