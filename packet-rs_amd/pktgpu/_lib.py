@@ -11,7 +11,8 @@ from . import schema
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libpktgpu.so")
+# PKTGPU_LIB overrides the library path (A/B builds of the same ABI in one session).
+LIB_PATH = os.environ.get("PKTGPU_LIB") or os.path.join(PKG_ROOT, "lib", "libpktgpu.so")
 
 
 class PktBatch(ctypes.Structure):
