@@ -260,6 +260,18 @@ int pkt_extract_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain
                        const pkt_field_spec_t *specs, uint32_t nspec,
                        uint64_t *const *values, uint8_t *const *found, void *stream);
 
+/* PacketSlice::to_vec / Packet::to_vec (packet.rs:733-740, 385-392) of every parsed packet:
+ * its header slices in LIST order, then its payload, written to dst + dst_offsets[i]
+ * (dst_offsets == NULL: the input batch's own layout, i*stride or offsets[i]).  With two or
+ * more GRE options the list order differs from wire order (Q2), so the bytes are reordered
+ * exactly as the reference's round trip reorders them.  `parsed` holds the chain columns of a
+ * pkt_parse_batch over the same batch (status, n_hdrs, hdr_type, hdr_off, payload_off,
+ * payload_len are read; the rest is ignored).  out_len[i] = bytes written (0 and nothing
+ * written for a packet whose status is not PKT_OK); out_len may be NULL. */
+int pkt_to_vec_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_out_t *parsed,
+                     uint8_t *dst, uint64_t dst_len, const uint64_t *dst_offsets,
+                     uint32_t *out_len, void *stream);
+
 /* Packet::ipv4_checksum (packet.rs:93-107) over n headers of 20 bytes at a fixed stride
  * in device memory: out[i] = checksum(hdrs + i*stride). */
 int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride, uint64_t n,

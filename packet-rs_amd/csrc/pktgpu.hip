@@ -284,6 +284,55 @@ __global__ __launch_bounds__(256) void extract_kernel(XParams p) {
     if (p.found) p.found[i] = hit >= 0 ? 1 : 0;
 }
 
+// PacketSlice::to_vec (packet.rs:733-740): header slices in list order, then the payload.
+struct TParams {
+    const uint8_t* slab;
+    uint64_t slab_len;
+    const uint64_t* offsets;
+    const uint32_t* lens;
+    uint32_t stride;
+    uint64_t n;
+    const uint8_t* status;
+    const uint8_t* n_hdrs;
+    const uint8_t* hdr_type;
+    const uint16_t* hdr_off;
+    const uint16_t* payload_off;
+    const uint16_t* payload_len;
+    uint8_t* dst;
+    uint64_t dst_len;
+    const uint64_t* dst_offsets;
+    uint32_t* out_len;
+};
+
+__constant__ uint8_t kHdrSize[PKT_HDR_COUNT] = {0, 14, 4, 20, 40, 4, 20, 8, 28, 8, 14, 3, 5, 4, 4, 4, 4, 8, 12, 8, 35, 4};
+
+__global__ __launch_bounds__(256) void to_vec_kernel(TParams p) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
+    uint64_t doff = p.dst_offsets ? p.dst_offsets[i] : off;
+    if (p.status[i] != PKT_OK) {
+        if (p.out_len) p.out_len[i] = 0;
+        return;
+    }
+    const uint8_t* src = p.slab + off;
+    uint64_t cur = doff;
+    const uint32_t nh = p.n_hdrs[i];
+    for (uint32_t j = 0; j < nh && j < PKT_MAX_HDRS; j++) {
+        const uint32_t t = p.hdr_type[(uint64_t)j * p.n + i];
+        const uint32_t o = p.hdr_off[(uint64_t)j * p.n + i];
+        const uint32_t sz = t < PKT_HDR_COUNT ? kHdrSize[t] : 0;
+        for (uint32_t k = 0; k < sz; k++)
+            if (cur + k < p.dst_len) p.dst[cur + k] = src[o + k];
+        cur += sz;
+    }
+    const uint32_t po = p.payload_off[i], pl = p.payload_len[i];
+    for (uint32_t k = 0; k < pl; k++)
+        if (cur + k < p.dst_len) p.dst[cur + k] = src[po + k];
+    cur += pl;
+    if (p.out_len) p.out_len[i] = (uint32_t)(cur - doff);
+}
+
 __global__ __launch_bounds__(256) void ipv4_csum_kernel(const uint8_t* hdrs, uint32_t stride, uint64_t n,
                                                         uint16_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -477,6 +526,41 @@ int pkt_extract_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* 
         e = hipGetLastError();
         if (e != hipSuccess) return hip_fail(ctx, e, "extract_kernel launch");
     }
+    return PKT_SUCCESS;
+}
+
+int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* parsed, uint8_t* dst,
+                     uint64_t dst_len, const uint64_t* dst_offsets, uint32_t* out_len, void* stream) {
+    if (!ctx || !b || !parsed) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (b->n == 0) return PKT_SUCCESS;
+    if (!b->slab || !dst || !parsed->status || !parsed->n_hdrs || !parsed->hdr_type || !parsed->hdr_off ||
+        !parsed->payload_off || !parsed->payload_len)
+        return fail(ctx, PKT_ERR_INVALID_ARG, "null slab/dst/chain column");
+    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
+    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    TParams tp;
+    tp.slab = b->slab;
+    tp.slab_len = b->slab_len;
+    tp.offsets = b->offsets;
+    tp.lens = b->lens;
+    tp.stride = b->stride;
+    tp.n = b->n;
+    tp.status = parsed->status;
+    tp.n_hdrs = parsed->n_hdrs;
+    tp.hdr_type = parsed->hdr_type;
+    tp.hdr_off = parsed->hdr_off;
+    tp.payload_off = parsed->payload_off;
+    tp.payload_len = parsed->payload_len;
+    tp.dst = dst;
+    tp.dst_len = dst_len;
+    tp.dst_offsets = dst_offsets;
+    tp.out_len = out_len;
+    hipLaunchKernelGGL(to_vec_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), tp);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
     return PKT_SUCCESS;
 }
 

@@ -180,6 +180,23 @@ class Parser:
                                                vp, fp, self._stream(stream)), "pkt_extract_fields")
         return vals, found
 
+    def to_vec(self, slab, parsed, stride=None, n=None, offsets=None, lens=None, dst=None,
+               dst_offsets=None, stream=None):
+        """PacketSlice::to_vec of every parsed packet into `dst` (default: a new buffer with
+        the input's layout).  Returns (dst, out_len)."""
+        torch = _torch()
+        b = self._batch(slab, n, stride, offsets, lens)
+        if dst is None:
+            dst = torch.zeros_like(slab)
+        out_len = torch.empty(b.n, dtype=torch.uint32, device=self.torch_device)
+        o = self.out_struct(parsed)
+        self._check(self._L.pkt_to_vec_batch(self._ctx, ctypes.byref(b), ctypes.byref(o),
+                                             ctypes.c_void_p(dst.data_ptr()), dst.numel(),
+                                             ctypes.c_void_p(dst_offsets.data_ptr() if dst_offsets is not None else 0),
+                                             ctypes.c_void_p(out_len.data_ptr()), self._stream(stream)),
+                    "pkt_to_vec_batch")
+        return dst, out_len
+
     def ipv4_checksum(self, hdrs, stride=20, n=None, stream=None):
         """Packet::ipv4_checksum over n 20-byte headers at a fixed stride (device u8 tensor)."""
         torch = _torch()

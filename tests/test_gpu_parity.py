@@ -314,3 +314,49 @@ def test_ipv4_checksum_batch_sweep(P):
     out = P.ipv4_checksum(dev(r), stride=24).cpu().numpy()
     want = np.array([oracle.ipv4_checksum(r[i, :20].tobytes()) for i in range(0, 50000, 50)])
     assert np.array_equal(out[::50], want)
+
+
+# ------------------------------------------------------------------ to_vec (config 1, Q2)
+def test_c1_roundtrip_to_vec(P):
+    """Config 1: 1 024 x 64 B parse + serialise round trip (tests/lib.rs:790-802 shape) on the
+    device: every packet's to_vec equals its bytes."""
+    n = 1024
+    slab = gen.gen_c2(n, seed=1).reshape(-1)
+    ds = dev(slab)
+    res = P.parse(ds, stride=64, columns=["chain"])
+    out, ln = P.to_vec(ds, res, stride=64)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), slab)
+    assert (ln.cpu().numpy() == 64).all()
+
+
+def test_to_vec_templates_and_gre_reorder_vs_oracle(P):
+    inner = gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                  "1.1.1.1", "2.2.2.2", 0, 64, 0, 0, [], 53, 1000, False, b"x" * 8)
+    inner.remove(0)
+    pkts = [p.to_vec() for p in gen.reference_22_packets()]
+    for c, k, s in ((1, 1, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0)):
+        pkts.append(gen.create_gre_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                          "3.3.3.3", "4.4.4.4", 0, 64, 0, 0, [], c, 0, k, s, 0, 0, 0,
+                                          0x1111, 0x2222, 0x33333333, 0x44444444, b"", inner).to_vec())
+    pkts.append(pkts[0][:30])  # truncated: not written
+    buf = b"".join(pkts)
+    lens = np.array([len(p) for p in pkts], np.uint32)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    slab = np.frombuffer(buf + bytes(16), np.uint8)
+    ds, do, dl = dev(slab), dev(offs), dev(lens)
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl)
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    reordered = 0
+    for i, p in enumerate(pkts):
+        try:
+            want = oracle.slow_parse_to_vec(p)
+        except ValueError:
+            assert ln[i] == 0
+            continue
+        got = o[offs[i]:offs[i] + ln[i]].tobytes()
+        assert got == want, i
+        reordered += got != p
+    assert reordered == 3  # the GRE packets with >= 2 options (Q2)
