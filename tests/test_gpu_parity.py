@@ -359,4 +359,4 @@ def test_to_vec_templates_and_gre_reorder_vs_oracle(P):
         got = o[offs[i]:offs[i] + ln[i]].tobytes()
         assert got == want, i
         reordered += got != p
-    assert reordered == 3  # the GRE packets with >= 2 options (Q2)
+    assert reordered == 4  # the four GRE packets, each with >= 2 options (Q2)
