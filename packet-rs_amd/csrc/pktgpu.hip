@@ -20,6 +20,7 @@ using namespace pktgpu;
 struct pkt_ctx {
     int device;
     uint32_t window;  // 0 = auto
+    int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
     std::string err;
 };
 
@@ -165,55 +166,121 @@ __device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint6
     if (len > 0xFFFFu) len = 0xFFFFu;  // u16 offsets/lengths in the ABI
 }
 
+// Chain-class key of a staged packet (6 bits): the EtherType after up to two VLAN tags and the
+// IP protocol behind it.  Packets with one key walk (nearly) the same states, so sorting a block
+// by key makes its waves walk one case per header instead of one per distinct state.
+__device__ __forceinline__ uint32_t class_key(const PacketView& pv, bool active) {
+    if (!active || pv.len < 14) return 63u;
+    uint32_t et = pv.be16(12), o = 14, v = 0;
+    if (et == 0x8100u && pv.len >= o + 4) { et = pv.be16(o + 2); o += 4; v = 1; }
+    if (et == 0x8100u && pv.len >= o + 4) { et = pv.be16(o + 2); o += 4; v = 2; }
+    uint32_t pr = 0;
+    if (et == 0x0800u && pv.len >= o + 10) pr = pv.u8(o + 9);
+    else if (et == 0x86DDu && pv.len >= o + 7) pr = pv.u8(o + 6);
+    const uint32_t cls = et < 1500u ? 0u : et == 0x0800u ? 1u : et == 0x86DDu ? 2u : et == 0x0806u ? 3u : 4u;
+    // protocol class: TCP, UDP, or "other next header" (GRE, ICMP, IP-in-IP); 0 = payload
+    const uint32_t pc = pr == 6u ? 1u : pr == 17u ? 2u
+                      : (pr == 47u || pr == 1u || pr == 58u || pr == 4u || pr == 41u) ? 3u : 0u;
+    return (cls * 3u + v) * 4u + pc;  // <= 59 for an active packet; 63 = inactive
+}
+
 template <int NCH, uint32_t GM>
 __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
-    // (NCH + 1) chunk rows per wave: the extra row is slack so a window read of dword k+1 never
-    // leaves this wave's region.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kWavesPerBlock][(NCH + 1) * kChunkRow];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wv = threadIdx.x / kWave;
-    const uint32_t i = blockIdx.x * (uint32_t)kBlock + threadIdx.x;  // within this launch
-    const bool active = i < p.n;
+    // Block-wide chunk-major window: chunk c of the block's packet q at c*kChunkRow + q*16
+    // (kChunkRow = 256 packets * 16 B).  (NCH + 1) rows: the extra row is slack so a window read
+    // of dword k+1 never leaves the block's region.
+    __shared__ __attribute__((aligned(16))) uint8_t lds[(NCH + 1) * kChunkRow];
+    __shared__ uint32_t s_hist[64];
+    __shared__ uint16_t s_perm[kBlock];
+    __shared__ uint32_t s_key0, s_mixed;
+    const uint32_t t = threadIdx.x;
+    const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
 
+    // ---- stage: lane t loads ITS packet's first NCH 16-byte chunks (from the 16-byte-aligned
+    // start) with per-lane dwordx4 loads (faster than the LDS-DMA gather, scripts/probe.py) and
+    // writes them with conflict-free ds_write_b128 (an 8-lane write group spans all banks).
+    // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
+    // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
+    {
+        const uint32_t i0 = base + t;
+        uint64_t off = 0;
+        uint32_t len = 0;
+        if (i0 < p.n) packet_range(p, i0, off, len);
+        const uint64_t a0 = off & ~(uint64_t)15;
+        const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 chunk[NCH];
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            uint64_t o = a0 + 16u * (uint32_t)c;
+            o = o > last16 ? last16 : o;
+            chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
+        }
+#pragma unroll
+        for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
+    }
+
+    // ---- optional in-block steering: counting sort of the block's packets by class_key
+    uint32_t q = t;  // the block-local packet this lane walks
+    if (p.sort) {
+        {
+            const uint32_t i0 = base + t;
+            uint64_t off = 0;
+            uint32_t len = 0;
+            if (i0 < p.n) packet_range(p, i0, off, len);
+            PacketView own;
+            own.lw = lds + t * 16;
+            own.slab = p.slab;
+            own.off = off;
+            own.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
+            own.shift = (uint32_t)(off & 15);
+            own.win_end = (uint32_t)NCH * 16u - own.shift;
+            own.len = len;
+            const uint32_t key = class_key(own, i0 < p.n);
+            if (t < 64) s_hist[t] = 0;
+            if (t == 0) { s_key0 = key; s_mixed = 0; }
+            __syncthreads();
+            if (key != s_key0) s_mixed = 1;
+            const uint32_t rank = atomicAdd(&s_hist[key], 1u);
+            __syncthreads();
+            if (s_mixed) {  // block-uniform
+                if (t < 64) {  // exclusive scan of the 64 bucket counts by wave 0
+                    const uint32_t v = s_hist[t];
+                    uint32_t x = v;
+#pragma unroll
+                    for (int d = 1; d < 64; d <<= 1) {
+                        const uint32_t y = __shfl_up(x, d, 64);
+                        if ((int)t >= d) x += y;
+                    }
+                    s_hist[t] = x - v;
+                }
+                __syncthreads();
+                s_perm[s_hist[key] + rank] = (uint16_t)t;
+                __syncthreads();
+                q = s_perm[t];
+            }
+        }
+    }
+
+    const uint32_t i = base + q;
+    const bool active = i < p.n;
     uint64_t off = 0;
     uint32_t len = 0;
     if (active) packet_range(p, i, off, len);
-
-    // ---- stage the first NCH*16 bytes (from the 16-byte-aligned start) of each packet.
-    // Per-lane dwordx4 loads of the packet's chunks (measured faster than the LDS-DMA gather
-    // for per-packet strides: scripts/probe.py), then conflict-free ds_write_b128 into the
-    // chunk-major window (lane l of row c at c*1024 + l*16: 8-lane write groups span all banks).
-    // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
-    // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
-    const uint64_t a0 = off & ~(uint64_t)15;
-    const uint32_t shift = (uint32_t)(off - a0);
-    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
-    uint8_t* win = &lds[wv][0];
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 chunk[NCH];
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-        uint64_t o = a0 + 16u * (uint32_t)c;
-        o = o > last16 ? last16 : o;
-        chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
-    }
-#pragma unroll
-    for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(win + c * kChunkRow + lane * 16) = chunk[c];
-    __builtin_amdgcn_wave_barrier();
-
     PacketView pv;
-    pv.lw = win + lane * 16;
+    pv.lw = lds + q * 16;
     pv.slab = p.slab;
     pv.off = off;
     pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
-    pv.shift = shift;
-    pv.win_end = (uint32_t)NCH * 16u - shift;
+    pv.shift = (uint32_t)(off & 15);
+    pv.win_end = (uint32_t)NCH * 16u - pv.shift;
     pv.len = len;
+    __builtin_amdgcn_wave_barrier();
 
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
-    auto push = [&](uint32_t slot, uint32_t t, uint32_t o) {
-        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)t;
+    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
+        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)ty;
         if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
     };
     WalkResult r;
@@ -411,6 +478,7 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
     pkt_ctx* c = new pkt_ctx();
     c->device = device;
     c->window = 0;
+    c->sort = 0;
     *out = c;
     return PKT_SUCCESS;
 }
@@ -425,6 +493,12 @@ const char* pkt_ctx_last_error(const pkt_ctx_t* ctx) { return ctx ? ctx->err.c_s
 int pkt_ctx_set_window(pkt_ctx_t* ctx, uint32_t w) {
     if (!ctx) return PKT_ERR_INVALID_ARG;
     ctx->window = w;
+    return PKT_SUCCESS;
+}
+
+int pkt_ctx_set_sort(pkt_ctx_t* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
+    ctx->sort = mode;
     return PKT_SUCCESS;
 }
 
@@ -470,6 +544,7 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
         kp.stride = b->stride;
         kp.n = (uint32_t)cnt;
         kp.entry = entry;
+        kp.sort = ctx->sort == 1 || (ctx->sort == 0 && b->offsets != nullptr);
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         static const uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,

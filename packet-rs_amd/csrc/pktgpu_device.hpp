@@ -26,7 +26,7 @@ namespace pktgpu {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kChunkRow = kWave * 16;  // bytes of one chunk row (one LDS-DMA instruction)
+constexpr int kChunkRow = kBlock * 16;  // bytes of one chunk row: chunk c of the block's 256 packets
 
 // Walk states = the parse_* functions of fast.rs (+ accept / done markers).
 enum State : uint32_t {
@@ -50,6 +50,7 @@ struct KParams {
     uint32_t stride;
     uint32_t n;
     int entry;
+    int sort;  // in-block counting sort by chain class before the walk
     pkt_out_t out;
 };
 
@@ -88,7 +89,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 // A lane's view of its packet: LDS window + global fallback.
 struct PacketView {
-    const uint8_t* lw;        // LDS window base of this wave (chunk-major), already + lane*16
+    const uint8_t* lw;        // LDS window of this packet: block window + q*16 (chunk-major)
     const uint8_t* slab;      // slab base (16-byte aligned)
     uint64_t off;             // packet start in the slab
     uint64_t last4;           // last readable aligned dword offset of the slab

@@ -94,6 +94,10 @@ class Parser:
     def set_window(self, window_bytes):
         self._L.pkt_ctx_set_window(self._ctx, int(window_bytes))
 
+    def set_sort(self, mode):
+        """0 = auto (indexed batches), 1 = always, 2 = never (see pkt_ctx_set_sort)."""
+        self._check(self._L.pkt_ctx_set_sort(self._ctx, int(mode)), "pkt_ctx_set_sort")
+
     def _check(self, rc, what):
         if rc != 0:
             msg = self._L.pkt_ctx_last_error(self._ctx)

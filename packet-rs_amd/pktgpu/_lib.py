@@ -55,6 +55,7 @@ SIGNATURES = {
     "pkt_ctx_destroy": (ctypes.c_int, [_P]),
     "pkt_ctx_last_error": (ctypes.c_char_p, [_P]),
     "pkt_ctx_set_window": (ctypes.c_int, [_P, ctypes.c_uint32]),
+    "pkt_ctx_set_sort": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
     "pkt_extract_fields": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
