@@ -247,8 +247,8 @@ const char *pkt_ctx_last_error(const pkt_ctx_t *ctx);
 int         pkt_ctx_set_window(pkt_ctx_t *ctx, uint32_t window_bytes);
 /* Tuning knob: before walking, sort each block of 256 packets by a chain-class key (EtherType
  * after VLAN tags, IP protocol) so each wave walks packets of one layout; outputs still land at
- * the packets' own indices.  0 = auto (on for indexed batches such as pcap replays, off for
- * fixed-stride slabs), 1 = always, 2 = never. */
+ * the packets' own indices.  0 = auto (currently: off — the barriers and result staging cost
+ * more than the uniform waves save on the measured mixes), 1 = always, 2 = never. */
 int         pkt_ctx_set_sort(pkt_ctx_t *ctx, int mode);
 
 /* ---- the hot path ---- */

@@ -184,17 +184,57 @@ __device__ __forceinline__ uint32_t class_key(const PacketView& pv, bool active)
     return (cls * 3u + v) * 4u + pc;  // <= 59 for an active packet; 63 = inactive
 }
 
+// Dynamic-LDS carve of a parse block (base 16-byte aligned; nothing static in front of it).
+//   [0, (NCH+1)*kChunkRow)   packet windows, chunk-major (chunk c of packet q at c*kChunkRow + q*16)
+//   sort part (p.sort only): bucket counts, permutation, the walk results of the 256 packets
+struct SortLds {
+    uint32_t hist[64];
+    uint32_t key0, mixed, pad[2];
+    uint16_t perm[kBlock];
+    uint8_t slot_type[PKT_MAX_HDRS][kBlock];
+    uint16_t slot_off[PKT_MAX_HDRS][kBlock];
+    uint8_t status[kBlock], n[kBlock];
+    uint16_t poff[kBlock];
+    uint32_t mask[kBlock];
+    int16_t first[6][kBlock];
+};
+
+__host__ __device__ constexpr size_t window_lds(int nch) { return (size_t)(nch + 1) * kChunkRow; }
+
+__device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
+                                                uint32_t len, int nch) {
+    PacketView pv;
+    pv.lw = lds + q * 16;
+    pv.slab = p.slab;
+    pv.off = off;
+    pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
+    pv.shift = (uint32_t)(off & 15);
+    pv.win_end = (uint32_t)nch * 16u - pv.shift;
+    pv.len = len;
+    return pv;
+}
+
+template <uint32_t GM>
+__device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uint32_t len, const WalkResult& r) {
+    const bool ok = r.status == PKT_OK;
+    if (want<GM, G_CHAIN>(out.status)) st<uint8_t>(out.status, i, (uint8_t)r.status);
+    if (want<GM, G_CHAIN>(out.n_hdrs)) st<uint8_t>(out.n_hdrs, i, ok ? (uint8_t)r.n : (uint8_t)0);
+    if (want<GM, G_CHAIN>(out.payload_off)) st<uint16_t>(out.payload_off, 2 * i, ok ? (uint16_t)r.payload_off : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.payload_len)) st<uint16_t>(out.payload_len, 2 * i, ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.hdr_mask)) st<uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
+}
+
 template <int NCH, uint32_t GM>
 __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
-    // Block-wide chunk-major window: chunk c of the block's packet q at c*kChunkRow + q*16
-    // (kChunkRow = 256 packets * 16 B).  (NCH + 1) rows: the extra row is slack so a window read
-    // of dword k+1 never leaves the block's region.
-    __shared__ __attribute__((aligned(16))) uint8_t lds[(NCH + 1) * kChunkRow];
-    __shared__ uint32_t s_hist[64];
-    __shared__ uint16_t s_perm[kBlock];
-    __shared__ uint32_t s_key0, s_mixed;
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    SortLds& S = *reinterpret_cast<SortLds*>(lds + window_lds(NCH));  // only touched if p.sort
     const uint32_t t = threadIdx.x;
     const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
+    const uint32_t i_own = base + t;
+    const bool active_own = i_own < p.n;
+    uint64_t off_own = 0;
+    uint32_t len_own = 0;
+    if (active_own) packet_range(p, i_own, off_own, len_own);
 
     // ---- stage: lane t loads ITS packet's first NCH 16-byte chunks (from the 16-byte-aligned
     // start) with per-lane dwordx4 loads (faster than the LDS-DMA gather, scripts/probe.py) and
@@ -202,11 +242,7 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
     // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
     // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
     {
-        const uint32_t i0 = base + t;
-        uint64_t off = 0;
-        uint32_t len = 0;
-        if (i0 < p.n) packet_range(p, i0, off, len);
-        const uint64_t a0 = off & ~(uint64_t)15;
+        const uint64_t a0 = off_own & ~(uint64_t)15;
         const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
         typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
         u32x4 chunk[NCH];
@@ -219,81 +255,98 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
 #pragma unroll
         for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
     }
-
-    // ---- optional in-block steering: counting sort of the block's packets by class_key
-    uint32_t q = t;  // the block-local packet this lane walks
-    if (p.sort) {
-        {
-            const uint32_t i0 = base + t;
-            uint64_t off = 0;
-            uint32_t len = 0;
-            if (i0 < p.n) packet_range(p, i0, off, len);
-            PacketView own;
-            own.lw = lds + t * 16;
-            own.slab = p.slab;
-            own.off = off;
-            own.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
-            own.shift = (uint32_t)(off & 15);
-            own.win_end = (uint32_t)NCH * 16u - own.shift;
-            own.len = len;
-            const uint32_t key = class_key(own, i0 < p.n);
-            if (t < 64) s_hist[t] = 0;
-            if (t == 0) { s_key0 = key; s_mixed = 0; }
-            __syncthreads();
-            if (key != s_key0) s_mixed = 1;
-            const uint32_t rank = atomicAdd(&s_hist[key], 1u);
-            __syncthreads();
-            if (s_mixed) {  // block-uniform
-                if (t < 64) {  // exclusive scan of the 64 bucket counts by wave 0
-                    const uint32_t v = s_hist[t];
-                    uint32_t x = v;
-#pragma unroll
-                    for (int d = 1; d < 64; d <<= 1) {
-                        const uint32_t y = __shfl_up(x, d, 64);
-                        if ((int)t >= d) x += y;
-                    }
-                    s_hist[t] = x - v;
-                }
-                __syncthreads();
-                s_perm[s_hist[key] + rank] = (uint16_t)t;
-                __syncthreads();
-                q = s_perm[t];
-            }
-        }
-    }
-
-    const uint32_t i = base + q;
-    const bool active = i < p.n;
-    uint64_t off = 0;
-    uint32_t len = 0;
-    if (active) packet_range(p, i, off, len);
-    PacketView pv;
-    pv.lw = lds + q * 16;
-    pv.slab = p.slab;
-    pv.off = off;
-    pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
-    pv.shift = (uint32_t)(off & 15);
-    pv.win_end = (uint32_t)NCH * 16u - pv.shift;
-    pv.len = len;
-    __builtin_amdgcn_wave_barrier();
-
+    const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
-    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
-        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)ty;
-        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
-    };
-    WalkResult r;
-    walk(pv, entry_state(p.entry), active, push, r);
-    if (!active) return;
 
-    const bool ok = r.status == PKT_OK;
-    if (want<GM, G_CHAIN>(out.status)) st<uint8_t>(out.status, i, (uint8_t)r.status);
-    if (want<GM, G_CHAIN>(out.n_hdrs)) st<uint8_t>(out.n_hdrs, i, ok ? (uint8_t)r.n : (uint8_t)0);
-    if (want<GM, G_CHAIN>(out.payload_off)) st<uint16_t>(out.payload_off, 2 * i, ok ? (uint16_t)r.payload_off : (uint16_t)0);
-    if (want<GM, G_CHAIN>(out.payload_len)) st<uint16_t>(out.payload_len, 2 * i, ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0);
-    if (want<GM, G_CHAIN>(out.hdr_mask)) st<uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
-    emit_fields<GM>(out, i, pv, r, ok);
+    if (!p.sort) {
+        // ---- unsorted: each lane walks and emits its own packet (no barrier: own LDS only)
+        __builtin_amdgcn_wave_barrier();
+        auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
+            if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i_own] = (uint8_t)ty;
+            if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i_own] = (uint16_t)o;
+        };
+        WalkResult r;
+        walk(pv_own, entry_state(p.entry), active_own, push, r);
+        if (!active_own) return;
+        emit_chain<GM>(out, i_own, len_own, r);
+        emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+        return;
+    }
+
+    // ---- sorted: counting sort of the block's packets by chain class (LDS atomics give each
+    // lane its rank in its bucket; wave 0 scans the 64 bucket counts), walk in sorted order so a
+    // wave holds one layout, stage the walk results in LDS, then every lane emits its OWN packet
+    // (coalesced stores at the packets' own indices).
+    const uint32_t key = class_key(pv_own, active_own);
+    if (t < 64) S.hist[t] = 0;
+    if (t == 0) { S.key0 = key; S.mixed = 0; }
+    __syncthreads();
+    if (key != S.key0) S.mixed = 1;
+    const uint32_t rank = atomicAdd(&S.hist[key], 1u);
+    __syncthreads();
+    uint32_t q = t;
+    if (S.mixed) {  // block-uniform
+        if (t < 64) {
+            const uint32_t v = S.hist[t];
+            uint32_t x = v;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t y = __shfl_up(x, d, 64);
+                if ((int)t >= d) x += y;
+            }
+            S.hist[t] = x - v;
+        }
+        __syncthreads();
+        S.perm[S.hist[key] + rank] = (uint16_t)t;
+        __syncthreads();
+        q = S.perm[t];
+    }
+    {
+        const uint32_t iq = base + q;
+        const bool aq = iq < p.n;
+        uint64_t offq = 0;
+        uint32_t lenq = 0;
+        if (aq) packet_range(p, iq, offq, lenq);
+        const PacketView pvq = make_view(p, lds, q, offq, lenq, NCH);
+        auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
+            S.slot_type[slot][q] = (uint8_t)ty;
+            S.slot_off[slot][q] = (uint16_t)o;
+        };
+        WalkResult r;
+        walk(pvq, entry_state(p.entry), aq, push, r);
+        S.status[q] = (uint8_t)r.status;
+        S.n[q] = (uint8_t)r.n;
+        S.poff[q] = (uint16_t)r.payload_off;
+        S.mask[q] = r.mask;
+        S.first[0][q] = (int16_t)r.f_eth;
+        S.first[1][q] = (int16_t)r.f_vlan;
+        S.first[2][q] = (int16_t)r.f_ipv4;
+        S.first[3][q] = (int16_t)r.f_ipv6;
+        S.first[4][q] = (int16_t)r.f_tcp;
+        S.first[5][q] = (int16_t)r.f_udp;
+    }
+    __syncthreads();
+    if (!active_own) return;
+    WalkResult r;
+    r.status = S.status[t];
+    r.n = S.n[t];
+    r.payload_off = S.poff[t];
+    r.mask = S.mask[t];
+    r.f_eth = S.first[0][t];
+    r.f_vlan = S.first[1][t];
+    r.f_ipv4 = S.first[2][t];
+    r.f_ipv6 = S.first[3][t];
+    r.f_tcp = S.first[4][t];
+    r.f_udp = S.first[5][t];
+    if (want<GM, G_CHAIN>(out.hdr_type) || want<GM, G_CHAIN>(out.hdr_off)) {
+        for (uint32_t j = 0; j < r.n; j++) {
+            if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)j * ns + i_own] = S.slot_type[j][t];
+            if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)j * ns + i_own] = S.slot_off[j][t];
+        }
+    }
+    emit_chain<GM>(out, i_own, len_own, r);
+    emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
 }
 
 // Batched `<Hdr>Slice::<field>()` (headers.rs:195-201 -> bit_range 252-263).
@@ -426,7 +479,8 @@ int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
 template <int NCH, uint32_t GM>
 hipError_t launch_parse(const KParams& kp, hipStream_t s) {
     dim3 grid((unsigned)((kp.n + kBlock - 1) / kBlock));
-    hipLaunchKernelGGL((parse_kernel<NCH, GM>), grid, dim3(kBlock), 0, s, kp);
+    const size_t lds = window_lds(NCH) + (kp.sort ? sizeof(SortLds) : 0);
+    hipLaunchKernelGGL((parse_kernel<NCH, GM>), grid, dim3(kBlock), lds, s, kp);
     return hipGetLastError();
 }
 
@@ -544,7 +598,8 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
         kp.stride = b->stride;
         kp.n = (uint32_t)cnt;
         kp.entry = entry;
-        kp.sort = ctx->sort == 1 || (ctx->sort == 0 && b->offsets != nullptr);
+        // auto = off: the sorted path measured slower on C3 and C4
+        kp.sort = ctx->sort == 1;
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         static const uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,

@@ -42,6 +42,7 @@ slabs = [base] + [base.clone() for _ in range(ring - 1)]
 d_offs = torch.from_numpy(offs).to(dev) if offs is not None else None
 d_lens = torch.from_numpy(lens).to(dev) if lens is not None else None
 
+stream = torch.cuda.current_stream()
 variants = []
 for w in [int(x) for x in args.windows.split(",")]:
     for v in args.variants.split(";"):
@@ -52,7 +53,12 @@ for w in [int(x) for x in args.windows.split(",")]:
         variants.append((f"w={w} cols={v}", w, bs, os_, cols, outs))
 
 copy_dst = [torch.empty_like(base) for _ in range(ring)]
-stream = torch.cuda.current_stream()
+# warm every variant (code-object load, first touch of its output ring, clocks)
+for name, w, bs, os_, cols, outs in variants:
+    P.set_window(w)
+    for k in range(2 * ring):
+        P.launch(bs[k % ring], 0, os_[k % ring], stream)
+torch.cuda.synchronize()
 res = {name: [] for name, *_ in variants}
 res["torch_copy"] = []
 for rnd in range(args.rounds):
@@ -80,6 +86,9 @@ P.set_window(0)
 import time
 for S in [int(x) for x in args.streams.split(",")]:
     streams = [torch.cuda.Stream() for _ in range(S)]
+    for k in range(64):  # first use of a new stream is slow: warm them
+        P.launch(variants[0][2][k % ring], 0, variants[0][3][k % ring], streams[k % S])
+    torch.cuda.synchronize()
     for name, w, bs, os_, cols, outs in variants:
         P.set_window(w)
         ts = []
