@@ -277,6 +277,22 @@ int pkt_to_vec_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_out_t *
                      uint8_t *dst, uint64_t dst_len, const uint64_t *dst_offsets,
                      uint32_t *out_len, void *stream);
 
+/* Batched header rewrite, in place in the slab (the slab of `batch` must be writable):
+ * `<Hdr>::set_<field>(v)` (headers.rs:340-344 -> set_bit_range 315-324) for each spec, in spec
+ * order, on the spec's header of every packet's chain.  The low (end-start+1) bits of
+ * values[s][i] go to bits [start..=end] (bits of a field wider than 64 above the value's 64
+ * bits become 0, as set_bit_range shifts the u64 right once per bit).  Packets whose chain lacks
+ * the header are untouched.  `values` is a HOST array of nspec DEVICE pointers ([n] each). */
+int pkt_set_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
+                   const pkt_field_spec_t *specs, uint32_t nspec, const uint64_t *const *values,
+                   void *stream);
+
+/* `ipv4.set_header_checksum(Packet::ipv4_checksum(ipv4.to_vec()))` (utils.rs:233-236;
+ * packet.rs:93-107 with the Q1 fold) on the `occurrence`-th IPv4 header of every packet, in
+ * place.  Packets without that header are untouched. */
+int pkt_ipv4_update_checksum(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
+                             uint32_t occurrence, void *stream);
+
 /* Packet::ipv4_checksum (packet.rs:93-107) over n headers of 20 bytes at a fixed stride
  * in device memory: out[i] = checksum(hdrs + i*stride). */
 int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride, uint64_t n,

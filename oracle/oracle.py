@@ -163,3 +163,45 @@ def slow_parse_to_vec(pkt, entry=0):
     if k < 0:
         raise ValueError(schema.STATUS_NAMES[-k])
     return buf.raw[:k]
+
+
+def set_bit_range(hdr, msb, lsb, value):
+    """headers.rs:315-324 on a bytearray (returns a new bytes)."""
+    a = (ctypes.c_uint8 * len(hdr)).from_buffer_copy(bytes(hdr))
+    lib().orc_set_bit_range.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_uint64]
+    lib().orc_set_bit_range(ctypes.addressof(a), msb, lsb, value)
+    return bytes(a)
+
+
+def _chain_struct(chain):
+    ch = PktChain()
+    nh = np.ascontiguousarray(chain["n_hdrs"], np.uint8)
+    ht = np.ascontiguousarray(chain["hdr_type"], np.uint8)
+    ho = np.ascontiguousarray(chain["hdr_off"], np.uint16)
+    ch.n_hdrs, ch.hdr_type, ch.hdr_off = nh.ctypes.data, ht.ctypes.data, ho.ctypes.data
+    return ch, (nh, ht, ho)
+
+
+def set_fields(slab, n, chain, specs, values, stride=None, offsets=None, lens=None):
+    """Oracle batched setters, in place on the numpy `slab` (must be writable, uint8)."""
+    assert slab.flags.writeable and slab.dtype == np.uint8 and slab.flags.c_contiguous
+    b, keep = _batch(slab, n, stride, offsets, lens)
+    ch, keep2 = _chain_struct(chain)
+    sp = (PktFieldSpec * max(1, len(specs)))()
+    for i, (t, occ, s, e) in enumerate(specs):
+        sp[i] = PktFieldSpec(t, occ, s, e, 0)
+    vals = [np.ascontiguousarray(v, np.uint64) for v in values]
+    vp = (ctypes.c_void_p * max(1, len(vals)))(*[v.ctypes.data for v in vals])
+    L = lib()
+    L.orc_set_fields.argtypes = [ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
+                                 ctypes.POINTER(PktFieldSpec), ctypes.c_uint32, ctypes.c_void_p]
+    L.orc_set_fields(ctypes.byref(b), ctypes.byref(ch), sp, len(specs), vp)
+
+
+def ipv4_update_checksum(slab, n, chain, occurrence=0, stride=None, offsets=None, lens=None):
+    assert slab.flags.writeable and slab.dtype == np.uint8 and slab.flags.c_contiguous
+    b, keep = _batch(slab, n, stride, offsets, lens)
+    ch, keep2 = _chain_struct(chain)
+    L = lib()
+    L.orc_ipv4_update_checksum.argtypes = [ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain), ctypes.c_uint32]
+    L.orc_ipv4_update_checksum(ctypes.byref(b), ctypes.byref(ch), occurrence)

@@ -675,3 +675,54 @@ long orc_slow_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out
     ps_free(&ps);
     return (long)k;
 }
+
+/* ------------------------------------------------------------------ header rewrite */
+/* headers.rs:315-324 — set_bit_range: for i in (lsb..=msb).rev(): bit i := value & 1;
+ * value >>= 1 (one bit at a time, with the lock-free slice here). */
+void orc_set_bit_range(uint8_t *map, size_t msb, size_t lsb, uint64_t value) {
+    const size_t bit_len = 8;
+    for (size_t i = msb + 1; i-- > lsb;) {
+        map[i / bit_len] &= (uint8_t)~(1u << (bit_len - i % bit_len - 1));
+        map[i / bit_len] |= (uint8_t)((value & 1) << (bit_len - i % bit_len - 1));
+        value >>= 1;
+    }
+}
+
+static int find_hdr(const pkt_chain_t *c, uint64_t n, uint64_t i, int type, int occurrence) {
+    int occ = 0;
+    for (int j = 0; j < c->n_hdrs[i]; j++)
+        if (c->hdr_type[(uint64_t)j * n + i] == type) {
+            if (occ == occurrence) return j;
+            occ++;
+        }
+    return -1;
+}
+
+/* Batched setters in spec order, in place (slab is written through b->slab). */
+int orc_set_fields(const pkt_batch_t *b, const pkt_chain_t *chain, const pkt_field_spec_t *specs,
+                   uint32_t nspec, const uint64_t *const *values) {
+    uint8_t *slab = (uint8_t *)b->slab;
+    for (uint64_t i = 0; i < b->n; i++) {
+        uint64_t off = b->offsets ? b->offsets[i] : i * (uint64_t)b->stride;
+        for (uint32_t s = 0; s < nspec; s++) {
+            int j = find_hdr(chain, b->n, i, specs[s].hdr_type, specs[s].occurrence);
+            if (j < 0) continue;
+            orc_set_bit_range(slab + off + chain->hdr_off[(uint64_t)j * b->n + i], specs[s].end,
+                              specs[s].start, values[s][i]);
+        }
+    }
+    return 0;
+}
+
+/* utils.rs:233-236: ipv4.set_header_checksum(Packet::ipv4_checksum(ipv4.to_vec())) */
+int orc_ipv4_update_checksum(const pkt_batch_t *b, const pkt_chain_t *chain, uint32_t occurrence) {
+    uint8_t *slab = (uint8_t *)b->slab;
+    for (uint64_t i = 0; i < b->n; i++) {
+        int j = find_hdr(chain, b->n, i, PKT_HDR_IPV4, (int)occurrence);
+        if (j < 0) continue;
+        uint64_t off = b->offsets ? b->offsets[i] : i * (uint64_t)b->stride;
+        uint8_t *h = slab + off + chain->hdr_off[(uint64_t)j * b->n + i];
+        orc_set_bit_range(h, 95, 80, orc_ipv4_checksum(h, 20));
+    }
+    return 0;
+}

@@ -18,6 +18,10 @@ int orc_parse_one(const uint8_t *p, size_t len, int entry, const pkt_out_t *out,
 int orc_parse_batch(const pkt_batch_t *b, int entry, const pkt_out_t *out, int nthreads);
 int orc_extract_fields(const pkt_batch_t *b, const pkt_chain_t *chain, const pkt_field_spec_t *specs,
                        uint32_t nspec, uint64_t *const *values, uint8_t *const *found);
+void orc_set_bit_range(uint8_t *map, size_t msb, size_t lsb, uint64_t value);
+int orc_set_fields(const pkt_batch_t *b, const pkt_chain_t *chain, const pkt_field_spec_t *specs,
+                   uint32_t nspec, const uint64_t *const *values);
+int orc_ipv4_update_checksum(const pkt_batch_t *b, const pkt_chain_t *chain, uint32_t occurrence);
 long orc_slow_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out, size_t cap);
 #ifdef __cplusplus
 }

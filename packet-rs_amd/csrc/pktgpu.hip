@@ -453,6 +453,81 @@ __global__ __launch_bounds__(256) void to_vec_kernel(TParams p) {
     if (p.out_len) p.out_len[i] = (uint32_t)(cur - doff);
 }
 
+// Batched set_bit_range (headers.rs:315-324) + in-place IPv4 checksum update.
+struct SParams {
+    uint8_t* slab;
+    uint64_t slab_len;
+    const uint64_t* offsets;
+    uint32_t stride;
+    uint64_t n;
+    const uint8_t* n_hdrs;
+    const uint8_t* hdr_type;
+    const uint16_t* hdr_off;
+};
+
+__device__ __forceinline__ int find_hdr(const SParams& p, uint64_t i, uint32_t type, uint32_t occurrence) {
+    const uint32_t nh = p.n_hdrs[i];
+    uint32_t occ = 0;
+    for (uint32_t j = 0; j < nh && j < PKT_MAX_HDRS; j++) {
+        if (p.hdr_type[(uint64_t)j * p.n + i] == type) {
+            if (occ == occurrence) return (int)j;
+            occ++;
+        }
+    }
+    return -1;
+}
+
+constexpr int kMaxSetSpecs = 16;
+struct SetSpecs {
+    pkt_field_spec_t spec[kMaxSetSpecs];
+    const uint64_t* values[kMaxSetSpecs];
+    uint32_t count;
+};
+
+__global__ __launch_bounds__(256) void set_fields_kernel(SParams p, SetSpecs ss) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
+    for (uint32_t s = 0; s < ss.count; s++) {
+        const int j = find_hdr(p, i, ss.spec[s].hdr_type, ss.spec[s].occurrence);
+        if (j < 0) continue;
+        uint8_t* h = p.slab + off + p.hdr_off[(uint64_t)j * p.n + i];
+        const uint32_t lsb = ss.spec[s].start, msb = ss.spec[s].end;
+        uint64_t v = ss.values[s][i];
+        // set_bit_range: bit msb gets value bit 0, then upwards; value >>= 1 each step.  Done a
+        // byte at a time from the last byte of the field backwards.
+        int32_t b = (int32_t)msb;
+        while (b >= (int32_t)lsb) {
+            const uint32_t byte = (uint32_t)b >> 3;
+            const int32_t lo = max((int32_t)lsb, (int32_t)(byte * 8));  // first field bit in this byte
+            const uint32_t nb = (uint32_t)(b - lo + 1);                  // field bits in this byte
+            const uint32_t sh = 7 - ((uint32_t)b & 7);                   // bit b's position from the LSB
+            const uint32_t m = (((1u << nb) - 1u) << sh) & 0xFFu;
+            const uint32_t bits = ((uint32_t)(v & ((1ull << nb) - 1ull)) << sh) & 0xFFu;
+            h[byte] = (uint8_t)((h[byte] & ~m) | bits);
+            v = nb >= 64 ? 0 : (v >> nb);
+            b = lo - 1;
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void ipv4_update_kernel(SParams p, uint32_t occurrence) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= p.n) return;
+    const int j = find_hdr(p, i, PKT_HDR_IPV4, occurrence);
+    if (j < 0) return;
+    const uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
+    uint8_t* h = p.slab + off + p.hdr_off[(uint64_t)j * p.n + i];
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 20; k += 2)
+        if (k != 10) s += ((uint32_t)h[k] << 8) | h[k + 1];
+    s = ((s >> 16) + s) & 0xFFFFu;
+    const uint32_t c = (~s) & 0xFFFFu;
+    h[10] = (uint8_t)(c >> 8);
+    h[11] = (uint8_t)c;
+}
+
 __global__ __launch_bounds__(256) void ipv4_csum_kernel(const uint8_t* hdrs, uint32_t stride, uint64_t n,
                                                         uint16_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -691,6 +766,71 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
                        reinterpret_cast<hipStream_t>(stream), tp);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
+    return PKT_SUCCESS;
+}
+
+static int sparams(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain, SParams& sp) {
+    if (!b->slab || !chain || !chain->n_hdrs || !chain->hdr_type || !chain->hdr_off)
+        return fail(ctx, PKT_ERR_INVALID_ARG, "null slab/chain column");
+    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
+    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
+    sp.slab = const_cast<uint8_t*>(b->slab);
+    sp.slab_len = b->slab_len;
+    sp.offsets = b->offsets;
+    sp.stride = b->stride;
+    sp.n = b->n;
+    sp.n_hdrs = chain->n_hdrs;
+    sp.hdr_type = chain->hdr_type;
+    sp.hdr_off = chain->hdr_off;
+    return PKT_SUCCESS;
+}
+
+int pkt_set_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
+                   const pkt_field_spec_t* specs, uint32_t nspec, const uint64_t* const* values,
+                   void* stream) {
+    if (!ctx || !b || (nspec && (!specs || !values))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (b->n == 0 || nspec == 0) return PKT_SUCCESS;
+    SParams sp;
+    int rc = sparams(ctx, b, chain, sp);
+    if (rc) return rc;
+    for (uint32_t s = 0; s < nspec; s++) {
+        const pkt_field_spec_t& f = specs[s];
+        if (f.hdr_type == 0 || f.hdr_type >= PKT_HDR_COUNT || f.end < f.start ||
+            f.end >= 8 * pkt_hdr_size(f.hdr_type) || !values[s])
+            return fail(ctx, PKT_ERR_INVALID_ARG, "bad field spec");
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    // specs are applied in order inside one thread per packet (overlapping specs behave as
+    // sequential setter calls); batches of kMaxSetSpecs per launch, launches ordered on the stream
+    for (uint32_t s0 = 0; s0 < nspec; s0 += kMaxSetSpecs) {
+        SetSpecs ss;
+        ss.count = std::min<uint32_t>(kMaxSetSpecs, nspec - s0);
+        for (uint32_t k = 0; k < ss.count; k++) {
+            ss.spec[k] = specs[s0 + k];
+            ss.values[k] = values[s0 + k];
+        }
+        hipLaunchKernelGGL(set_fields_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
+                           reinterpret_cast<hipStream_t>(stream), sp, ss);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(ctx, e, "set_fields_kernel launch");
+    }
+    return PKT_SUCCESS;
+}
+
+int pkt_ipv4_update_checksum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
+                             uint32_t occurrence, void* stream) {
+    if (!ctx || !b) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (b->n == 0) return PKT_SUCCESS;
+    SParams sp;
+    int rc = sparams(ctx, b, chain, sp);
+    if (rc) return rc;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipLaunchKernelGGL(ipv4_update_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), sp, occurrence);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "ipv4_update_kernel launch");
     return PKT_SUCCESS;
 }
 

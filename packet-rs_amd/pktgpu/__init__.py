@@ -201,6 +201,35 @@ class Parser:
                     "pkt_to_vec_batch")
         return dst, out_len
 
+    def _chain(self, chain):
+        ch = self._lib.PktChain()
+        ch.n_hdrs = chain["n_hdrs"].data_ptr()
+        ch.hdr_type = chain["hdr_type"].data_ptr()
+        ch.hdr_off = chain["hdr_off"].data_ptr()
+        return ch
+
+    def set_fields(self, slab, chain, specs, values, stride=None, n=None, offsets=None, lens=None,
+                   stream=None):
+        """In-place batched `<Hdr>::set_<field>(v)`: specs = [(hdr_type|name, occurrence, start,
+        end)], values = one uint64 device tensor per spec."""
+        b = self._batch(slab, n, stride, offsets, lens)
+        k = len(specs)
+        sp = (self._lib.PktFieldSpec * max(1, k))()
+        for i, (t, occ, s, e) in enumerate(specs):
+            t = HDR_ID[t] if isinstance(t, str) else int(t)
+            sp[i] = self._lib.PktFieldSpec(t, occ, s, e, 0)
+        vp = (ctypes.c_void_p * max(1, k))(*[v.data_ptr() for v in values])
+        self._check(self._L.pkt_set_fields(self._ctx, ctypes.byref(b), ctypes.byref(self._chain(chain)),
+                                           sp, k, vp, self._stream(stream)), "pkt_set_fields")
+
+    def ipv4_update_checksum(self, slab, chain, occurrence=0, stride=None, n=None, offsets=None,
+                             lens=None, stream=None):
+        """In-place: the occurrence-th IPv4 header's checksum := Packet::ipv4_checksum(header)."""
+        b = self._batch(slab, n, stride, offsets, lens)
+        self._check(self._L.pkt_ipv4_update_checksum(self._ctx, ctypes.byref(b),
+                                                     ctypes.byref(self._chain(chain)), occurrence,
+                                                     self._stream(stream)), "pkt_ipv4_update_checksum")
+
     def ipv4_checksum(self, hdrs, stride=20, n=None, stream=None):
         """Packet::ipv4_checksum over n 20-byte headers at a fixed stride (device u8 tensor)."""
         torch = _torch()
