@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <type_traits>
 
 #include "pktgpu_device.hpp"
 
@@ -42,7 +43,12 @@ __device__ __forceinline__ bool want(const void* p) {
 // Store at a 32-bit byte offset from a column base (global_store ... saddr: one VGPR offset).
 template <class T>
 __device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
-    *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff) = v;
+#if PKTGPU_NT_STORE
+    if constexpr (std::is_integral<T>::value)
+        __builtin_nontemporal_store(v, reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff));
+    else
+#endif
+        *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff) = v;
 }
 
 // Fields of the first header of each group (Q11), from the walk's first offsets.
@@ -250,7 +256,11 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
         for (int c = 0; c < NCH; c++) {
             uint64_t o = a0 + 16u * (uint32_t)c;
             o = o > last16 ? last16 : o;
+#if PKTGPU_NT_LOAD
+            chunk[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p.slab + o));
+#else
             chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
+#endif
         }
 #pragma unroll
         for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
