@@ -293,6 +293,13 @@ int pkt_set_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *
 int pkt_ipv4_update_checksum(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
                              uint32_t occurrence, void *stream);
 
+/* Batched packet generation, clone step (`pkt.clone().to_vec()` of tests/lib.rs:770-776 for n
+ * copies): writes the `len`-byte DEVICE packet `src` n times, at dst + i*stride, and zero-fills
+ * the rest of each stride slot.  Follow with pkt_parse_batch (chain), pkt_set_fields and
+ * pkt_ipv4_update_checksum to vary fields per packet (the update+clone workload, 778-787). */
+int pkt_broadcast(pkt_ctx_t *ctx, const uint8_t *src, uint32_t len, uint64_t n, uint32_t stride,
+                  uint8_t *dst, void *stream);
+
 /* Packet::ipv4_checksum (packet.rs:93-107) over n headers of 20 bytes at a fixed stride
  * in device memory: out[i] = checksum(hdrs + i*stride). */
 int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride, uint64_t n,

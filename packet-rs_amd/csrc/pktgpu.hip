@@ -538,6 +538,22 @@ __global__ __launch_bounds__(256) void ipv4_update_kernel(SParams p, uint32_t oc
     h[11] = (uint8_t)c;
 }
 
+// n copies of one packet at a fixed stride, 16 bytes per lane per step (slot-contiguous).
+__global__ __launch_bounds__(256) void broadcast_kernel(const uint8_t* src, uint32_t len, uint64_t n,
+                                                        uint32_t stride, uint8_t* dst) {
+    const uint64_t total = n * (uint64_t)stride;  // bytes, multiple of 16 (checked by the host)
+    for (uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; q < total;
+         q += (uint64_t)gridDim.x * blockDim.x * 16) {
+        const uint32_t o = (uint32_t)(q % stride);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        u32x4 v;
+        uint8_t* b = reinterpret_cast<uint8_t*>(&v);
+#pragma unroll
+        for (int k = 0; k < 16; k++) b[k] = (o + k < len) ? src[o + k] : (uint8_t)0;
+        *reinterpret_cast<u32x4*>(dst + q) = v;
+    }
+}
+
 __global__ __launch_bounds__(256) void ipv4_csum_kernel(const uint8_t* hdrs, uint32_t stride, uint64_t n,
                                                         uint16_t* out) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -841,6 +857,23 @@ int pkt_ipv4_update_checksum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_cha
                        reinterpret_cast<hipStream_t>(stream), sp, occurrence);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "ipv4_update_kernel launch");
+    return PKT_SUCCESS;
+}
+
+int pkt_broadcast(pkt_ctx_t* ctx, const uint8_t* src, uint32_t len, uint64_t n, uint32_t stride,
+                  uint8_t* dst, void* stream) {
+    if (!ctx || (n && (!src || !dst))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (n == 0) return PKT_SUCCESS;
+    if (stride == 0 || stride % 16 || len > stride || ((uintptr_t)dst & 15))
+        return fail(ctx, PKT_ERR_INVALID_ARG, "stride must be a non-zero multiple of 16 >= len, dst 16-byte aligned");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    const uint64_t chunks = n * (uint64_t)stride / 16;
+    const unsigned grid = (unsigned)std::min<uint64_t>((chunks + 255) / 256, 256u * 64u);
+    hipLaunchKernelGGL(broadcast_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
+                       src, len, n, stride, dst);
+    e = hipGetLastError();
+    if (e != hipSuccess) return hip_fail(ctx, e, "broadcast_kernel launch");
     return PKT_SUCCESS;
 }
 

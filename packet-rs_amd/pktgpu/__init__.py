@@ -230,6 +230,16 @@ class Parser:
                                                      ctypes.byref(self._chain(chain)), occurrence,
                                                      self._stream(stream)), "pkt_ipv4_update_checksum")
 
+    def broadcast(self, src, n, stride, dst=None, stream=None):
+        """n clones of the device packet `src` (uint8 tensor) at `stride` -> flat uint8 slab."""
+        torch = _torch()
+        if dst is None:
+            dst = torch.empty(n * stride, dtype=torch.uint8, device=self.torch_device)
+        self._check(self._L.pkt_broadcast(self._ctx, ctypes.c_void_p(src.data_ptr()), src.numel(), n,
+                                          stride, ctypes.c_void_p(dst.data_ptr()), self._stream(stream)),
+                    "pkt_broadcast")
+        return dst
+
     def ipv4_checksum(self, hdrs, stride=20, n=None, stream=None):
         """Packet::ipv4_checksum over n 20-byte headers at a fixed stride (device u8 tensor)."""
         torch = _torch()

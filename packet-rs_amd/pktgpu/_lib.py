@@ -68,6 +68,7 @@ SIGNATURES = {
                                       ctypes.POINTER(_P), _P]),
     "pkt_ipv4_update_checksum": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
                                                 ctypes.c_uint32, _P]),
+    "pkt_broadcast": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, _P, _P]),
     "pkt_ipv4_checksum_batch": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, _P, _P]),
     "pkt_pcap_index": (ctypes.c_int, [_P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64)]),
