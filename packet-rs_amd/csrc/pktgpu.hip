@@ -205,12 +205,25 @@ struct SortLds {
     int16_t first[6][kBlock];
 };
 
+#if PKTGPU_LDS_PACKED
+// packet-major: packet q's window at q * lane_stride, lane_stride = 4*NCH+1 dwords (odd, so the
+// per-lane dword reads of the walk hit 64 distinct banks); +16 B for the last lane's over-read
+__host__ __device__ constexpr uint32_t lane_stride(int nch) { return (uint32_t)(4 * nch + 1) * 4u; }
+__host__ __device__ constexpr size_t window_lds(int nch) {
+    return ((size_t)kBlock * lane_stride(nch) + 16 + 15) & ~(size_t)15;
+}
+#else
 __host__ __device__ constexpr size_t window_lds(int nch) { return (size_t)(nch + 1) * kChunkRow; }
+#endif
 
 __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
                                                 uint32_t len, int nch) {
     PacketView pv;
+#if PKTGPU_LDS_PACKED
+    pv.lw = lds + q * lane_stride(nch);
+#else
     pv.lw = lds + q * 16;
+#endif
     pv.slab = p.slab;
     pv.off = off;
     pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
@@ -263,7 +276,17 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
 #endif
         }
 #pragma unroll
-        for (int c = 0; c < NCH; c++) *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
+        for (int c = 0; c < NCH; c++) {
+#if PKTGPU_LDS_PACKED
+            uint32_t* w = reinterpret_cast<uint32_t*>(lds + t * lane_stride(NCH)) + 4 * c;
+            w[0] = chunk[c].x;
+            w[1] = chunk[c].y;
+            w[2] = chunk[c].z;
+            w[3] = chunk[c].w;
+#else
+            *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
+#endif
+        }
     }
     const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
     const pkt_out_t& out = p.out;

@@ -21,6 +21,13 @@
 
 #include "../../include/pktgpu.h"
 
+// LDS window layout.  1 (default): packet-major, odd lane stride (conflict-free per-lane dword
+// reads; C4 -3 %, C2/C3 neutral, scripts/ab_bench.sh).  0: chunk-major (ds_write_b128 staging,
+// 4-way bank conflicts on the walk's dword reads).
+#ifndef PKTGPU_LDS_PACKED
+#define PKTGPU_LDS_PACKED 1
+#endif
+
 namespace pktgpu {
 
 constexpr int kWave = 64;
@@ -99,7 +106,11 @@ struct PacketView {
 
     // aligned dword k of the window
     __device__ __forceinline__ uint32_t wdw(uint32_t k) const {
+#if PKTGPU_LDS_PACKED
+        return reinterpret_cast<const uint32_t*>(lw)[k];
+#else
         return *reinterpret_cast<const uint32_t*>(lw + (k >> 2) * kChunkRow + (k & 3) * 4);
+#endif
     }
     // aligned dword of the slab containing slab byte a (clamped to the readable end)
     __device__ __forceinline__ uint32_t gdw(uint64_t a) const {
@@ -297,8 +308,13 @@ __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool 
     for (;;) {
         const uint64_t pend = __ballot(L.live);
         if (pend == 0) break;
-        const uint32_t s0 = __builtin_amdgcn_readlane(L.st, (uint32_t)__builtin_ctzll(pend));
-        if (L.live && L.st == s0) {
+        uint32_t s0 = __builtin_amdgcn_readlane(L.st, (uint32_t)__builtin_ctzll(pend));
+        const bool mine = L.live && L.st == s0;
+        // Make s0 opaque: inside `mine` the compiler would otherwise substitute the lane's own
+        // (VGPR) state for s0 and turn the uniform scalar switch into a divergent compare tree
+        // with an exec-mask save/restore per level.
+        asm volatile("" : "+s"(s0));
+        if (mine) {
             // at most PKT_MAX_HDRS headers + parse + accept + the failing step
             if (++L.steps > PKT_MAX_HDRS + 3) {
                 fail(L, PKT_DEPTH_LIMIT);
