@@ -46,6 +46,8 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
+    ap.add_argument("--fastpath", type=int, default=int(os.environ.get("PKTGPU_FASTPATH", "1")),
+                    help="register fast path for Ether/IPv4/UDP|TCP (pkt_ctx_set_fastpath)")
     ap.add_argument("--streams", type=int, default=2,
                     help="consecutive steps are issued round-robin on this many HIP streams")
     return ap.parse_args()
@@ -121,6 +123,7 @@ def main():
     import pktgpu
     from pktgpu import schema
     P = pktgpu.Parser(gpu)
+    P.set_fastpath(args.fastpath)
     default_cols = {"c2": "chain,ether,ipv4,udp", "c3": "chain,ether,vlan,ipv4,tcp,udp",
                     "c4": "all", "c5": "chain,ether,ipv4,udp"}[args.config]
     if args.columns is None:

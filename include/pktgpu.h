@@ -108,6 +108,9 @@ typedef enum pkt_entry {
  *    lens[i] when lens != NULL, else `stride`.
  *  - Indexed slab (e.g. a pcap file copied as-is): offsets[i] / lens[i] (both required)
  *    give each packet's byte range inside the slab.
+ *  - A packet is the bytes of that range that lie inside [slab, slab + slab_len): its length
+ *    is clamped to the slab end (a slot past the end is an empty packet) and to 65535 (the
+ *    u16 offset/length columns).
  * The slab pointer must be 16-byte aligned; the kernels may read up to 15 bytes past a
  * packet's end but never past round_up(slab + slab_len, 16) (always inside a hipMalloc /
  * torch allocation, whose granularity is >= 256 B). */
@@ -250,12 +253,33 @@ int         pkt_ctx_set_window(pkt_ctx_t *ctx, uint32_t window_bytes);
  * the packets' own indices.  0 = auto (currently: off — the barriers and result staging cost
  * more than the uniform waves save on the measured mixes), 1 = always, 2 = never. */
 int         pkt_ctx_set_sort(pkt_ctx_t *ctx, int mode);
+/* Fast path (default on).  For entries PARSE and ETHERNET, a packet that starts on a 16-byte
+ * boundary and whose first bytes read Ether(0x0800) / IPv4 / UDP (dst != 4789) or TCP, long
+ * enough for every header, has its chain decided by three compares on the registers its bytes
+ * were loaded into, so it skips the walk.  Results are identical to the walk's (the same fast.rs
+ * path; the parity tests run with it forced on and off).  0 = off, 1 = on. */
+int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
 
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
  * Asynchronous on `stream`; returns after the launch. */
 int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
                     const pkt_out_t *out, void *stream);
+
+/* ---- host-memory path ----
+ * The reference's path starts and ends in host memory (a pcap file, a NIC ring).  One call moves
+ * a HOST batch through the device: `batch` (slab, offsets, lens) and `out` (column pointers, the
+ * pkt_out_t layout of pkt_parse_batch with slot columns strided by batch->n) are host memory.
+ * The batch is cut into chunks of `chunk` packets (0 = 262144) pipelined over three streams of
+ * the ctx: the copy-in of chunk k+1 and the copy-out of chunk k-1 overlap the parse of chunk k.
+ * Indexed chunks copy the byte span their records cover.  Host buffers from pkt_host_alloc
+ * (pinned) move at link rate; pageable ones work, staged by the runtime.  Blocks until every
+ * output is in host memory.  One host call at a time per ctx. */
+int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pkt_out_t *out,
+                   uint64_t chunk);
+/* Pinned (page-locked) host memory for pkt_parse_host buffers. */
+int pkt_host_alloc(pkt_ctx_t *ctx, uint64_t bytes, void **p);
+int pkt_host_free(pkt_ctx_t *ctx, void *p);
 
 /* Batched make_header! getter: for each spec s and packet i, values[s][i] = the field of
  * the chain's matching header (0 and found[s][i] = 0 when absent).  `values` and `found`

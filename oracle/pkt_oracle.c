@@ -545,14 +545,22 @@ static void fill_fields(const pkt_out_t *out, uint64_t i, const uint8_t *p, cons
 #undef G
 }
 
+/* Packet i of a batch (include/pktgpu.h, pkt_batch_t): its range clamped to the slab end and to
+ * 65535 bytes.  This is the batch ABI's framing, not part of the reference's algorithm. */
 static void packet_bounds(const pkt_batch_t *b, uint64_t i, const uint8_t **p, size_t *len) {
+    uint64_t off, l;
     if (b->offsets) {
-        *p = b->slab + b->offsets[i];
-        *len = b->lens[i];
+        off = b->offsets[i];
+        l = b->lens[i];
     } else {
-        *p = b->slab + i * (uint64_t)b->stride;
-        *len = b->lens ? b->lens[i] : b->stride;
+        off = i * (uint64_t)b->stride;
+        l = b->lens ? b->lens[i] : b->stride;
     }
+    uint64_t room = off < b->slab_len ? b->slab_len - off : 0;
+    if (l > room) l = room;
+    if (l > 0xFFFF) l = 0xFFFF;
+    *p = b->slab + (off < b->slab_len ? off : 0);
+    *len = (size_t)l;
 }
 
 int orc_parse_one(const uint8_t *p, size_t len, int entry, const pkt_out_t *out, uint64_t i, uint64_t n) {

@@ -18,10 +18,24 @@
 
 using namespace pktgpu;
 
+// Device buffers and streams of the host-memory pipeline (pkt_parse_host), grown on demand.
+struct HostPipe {
+    static constexpr int kSlots = 3;
+    bool init = false;
+    hipStream_t s[kSlots] = {};
+    uint8_t* slab[kSlots] = {};
+    uint64_t* offs[kSlots] = {};
+    uint32_t* lens[kSlots] = {};
+    uint8_t* out[kSlots] = {};
+    uint64_t slab_cap = 0, pkt_cap = 0, out_cap = 0;  // bytes per slot (pkt_cap: offs and lens)
+};
+
 struct pkt_ctx {
     int device;
+    HostPipe hp;
     uint32_t window;  // 0 = auto
     int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
+    int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     std::string err;
 };
 
@@ -53,15 +67,15 @@ __device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
 
 // Fields of the first header of each group (Q11), from the walk's first offsets.
 // `i` is the packet index within this launch (< 2^28, so every byte offset fits 32 bits).
-template <uint32_t GM>
-__device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, const PacketView& pv,
+template <uint32_t GM, class View>
+__device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, const View& pv,
                                             const WalkResult& r, bool ok) {
     const uint32_t o1 = i, o2 = i * 2u, o4 = i * 4u, o8 = i * 8u, o16 = i * 16u;
     // Ether (headers.rs:530-540): dst 0-47, src 48-95, etype 96-111
     if (want<GM, G_ETHER>(out.eth_dst) || want<GM, G_ETHER>(out.eth_src) || want<GM, G_ETHER>(out.eth_etype)) {
         uint32_t d[4] = {0, 0, 0, 0};
         const bool h = ok && r.f_eth >= 0;
-        if (h) pv.hdr<4>((uint32_t)r.f_eth, 14, d);
+        if (h) pv.template hdr<4>((uint32_t)r.f_eth, 14, d);
         if (want<GM, G_ETHER>(out.eth_dst)) st<uint64_t>(out.eth_dst, o8, ((uint64_t)d[0] << 16) | (d[1] >> 16));
         if (want<GM, G_ETHER>(out.eth_src)) st<uint64_t>(out.eth_src, o8, ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[2]);
         if (want<GM, G_ETHER>(out.eth_etype)) st<uint16_t>(out.eth_etype, o2, (uint16_t)(d[3] >> 16));
@@ -70,7 +84,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
     if (want<GM, G_VLAN>(out.vlan_pcp) || want<GM, G_VLAN>(out.vlan_cfi) || want<GM, G_VLAN>(out.vlan_vid) ||
         want<GM, G_VLAN>(out.vlan_etype)) {
         uint32_t d[1] = {0};
-        if (ok && r.f_vlan >= 0) pv.hdr<1>((uint32_t)r.f_vlan, 4, d);
+        if (ok && r.f_vlan >= 0) pv.template hdr<1>((uint32_t)r.f_vlan, 4, d);
         if (want<GM, G_VLAN>(out.vlan_pcp)) st<uint8_t>(out.vlan_pcp, o1, (uint8_t)(d[0] >> 29));
         if (want<GM, G_VLAN>(out.vlan_cfi)) st<uint8_t>(out.vlan_cfi, o1, (uint8_t)((d[0] >> 28) & 1u));
         if (want<GM, G_VLAN>(out.vlan_vid)) st<uint16_t>(out.vlan_vid, o2, (uint16_t)((d[0] >> 16) & 0xFFFu));
@@ -84,7 +98,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         want<GM, G_IPV4>(out.ipv4_src) || want<GM, G_IPV4>(out.ipv4_dst) || want<GM, G_IPV4>(out.ipv4_csum_calc)) {
         uint32_t d[5] = {0, 0, 0, 0, 0};
         const bool h = ok && r.f_ipv4 >= 0;
-        if (h) pv.hdr<5>((uint32_t)r.f_ipv4, 20, d);
+        if (h) pv.template hdr<5>((uint32_t)r.f_ipv4, 20, d);
         if (want<GM, G_IPV4>(out.ipv4_version)) st<uint8_t>(out.ipv4_version, o1, (uint8_t)(d[0] >> 28));
         if (want<GM, G_IPV4>(out.ipv4_ihl)) st<uint8_t>(out.ipv4_ihl, o1, (uint8_t)((d[0] >> 24) & 0xFu));
         if (want<GM, G_IPV4>(out.ipv4_diffserv)) st<uint8_t>(out.ipv4_diffserv, o1, (uint8_t)((d[0] >> 16) & 0xFFu));
@@ -111,7 +125,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         want<GM, G_IPV6>(out.ipv6_next_hdr) || want<GM, G_IPV6>(out.ipv6_hop_limit) ||
         want<GM, G_IPV6>(out.ipv6_src) || want<GM, G_IPV6>(out.ipv6_dst)) {
         uint32_t d[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
-        if (ok && r.f_ipv6 >= 0) pv.hdr<10>((uint32_t)r.f_ipv6, 40, d);
+        if (ok && r.f_ipv6 >= 0) pv.template hdr<10>((uint32_t)r.f_ipv6, 40, d);
         if (want<GM, G_IPV6>(out.ipv6_version)) st<uint8_t>(out.ipv6_version, o1, (uint8_t)(d[0] >> 28));
         if (want<GM, G_IPV6>(out.ipv6_traffic_class)) st<uint8_t>(out.ipv6_traffic_class, o1, (uint8_t)((d[0] >> 20) & 0xFFu));
         if (want<GM, G_IPV6>(out.ipv6_flow_label)) st<uint32_t>(out.ipv6_flow_label, o4, d[0] & 0xFFFFFu);
@@ -131,7 +145,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         want<GM, G_TCP>(out.tcp_flags) || want<GM, G_TCP>(out.tcp_window) || want<GM, G_TCP>(out.tcp_checksum) ||
         want<GM, G_TCP>(out.tcp_urgent_ptr)) {
         uint32_t d[5] = {0, 0, 0, 0, 0};
-        if (ok && r.f_tcp >= 0) pv.hdr<5>((uint32_t)r.f_tcp, 20, d);
+        if (ok && r.f_tcp >= 0) pv.template hdr<5>((uint32_t)r.f_tcp, 20, d);
         if (want<GM, G_TCP>(out.tcp_src)) st<uint16_t>(out.tcp_src, o2, (uint16_t)(d[0] >> 16));
         if (want<GM, G_TCP>(out.tcp_dst)) st<uint16_t>(out.tcp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
         if (want<GM, G_TCP>(out.tcp_seq_no)) st<uint32_t>(out.tcp_seq_no, o4, d[1]);
@@ -147,7 +161,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
     if (want<GM, G_UDP>(out.udp_src) || want<GM, G_UDP>(out.udp_dst) || want<GM, G_UDP>(out.udp_length) ||
         want<GM, G_UDP>(out.udp_checksum)) {
         uint32_t d[2] = {0, 0};
-        if (ok && r.f_udp >= 0) pv.hdr<2>((uint32_t)r.f_udp, 8, d);
+        if (ok && r.f_udp >= 0) pv.template hdr<2>((uint32_t)r.f_udp, 8, d);
         if (want<GM, G_UDP>(out.udp_src)) st<uint16_t>(out.udp_src, o2, (uint16_t)(d[0] >> 16));
         if (want<GM, G_UDP>(out.udp_dst)) st<uint16_t>(out.udp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
         if (want<GM, G_UDP>(out.udp_length)) st<uint16_t>(out.udp_length, o2, (uint16_t)(d[1] >> 16));
@@ -160,7 +174,7 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
 __device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint64_t& off,
                                              uint32_t& len) {
     if (p.offsets) {
-        off = p.offsets[i];
+        off = p.offsets[i] - p.off_bias;
         len = p.lens[i];
     } else {
         off = (p.i0 + i) * (uint64_t)p.stride;
@@ -244,7 +258,17 @@ __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uin
 }
 
 template <int NCH, uint32_t GM>
-__global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
+#ifndef PKTGPU_FAST_REG
+// 1: waves whose packets all take the fast path decode from registers, no LDS.  0 (default):
+// they stage and emit through LDS like mixed waves.  C2, same box: registers 28.7 us isolated /
+// 24.0 us pipelined per step, LDS 29.8 / 23.4 — the pipelined rate is the bench's value.
+#define PKTGPU_FAST_REG 0
+#endif
+#ifndef PKTGPU_WAVES_PER_EU
+#define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
+void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     SortLds& S = *reinterpret_cast<SortLds*>(lds + window_lds(NCH));  // only touched if p.sort
     const uint32_t t = threadIdx.x;
@@ -260,11 +284,11 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
     // writes them with conflict-free ds_write_b128 (an 8-lane write group spans all banks).
     // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
     // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    u32x4 chunk[NCH];
     {
         const uint64_t a0 = off_own & ~(uint64_t)15;
         const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        u32x4 chunk[NCH];
 #pragma unroll
         for (int c = 0; c < NCH; c++) {
             uint64_t o = a0 + 16u * (uint32_t)c;
@@ -275,33 +299,88 @@ __global__ __launch_bounds__(kBlock) void parse_kernel(KParams p) {
             chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
 #endif
         }
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-#if PKTGPU_LDS_PACKED
-            uint32_t* w = reinterpret_cast<uint32_t*>(lds + t * lane_stride(NCH)) + 4 * c;
-            w[0] = chunk[c].x;
-            w[1] = chunk[c].y;
-            w[2] = chunk[c].z;
-            w[3] = chunk[c].w;
-#else
-            *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
-#endif
+    }
+    // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose bytes 12-13 = 0x0800,
+    // byte 23 = 17 with bytes 36-37 != 4789 and len >= 42, or byte 23 = 6 and len >= 54, takes
+    // exactly fast.rs's Ether -> IPv4 -> UDP|TCP -> accept path (no bound or depth check can
+    // fail), so it needs neither the LDS window nor the walk.
+    bool fast = false;
+    if constexpr (NCH >= 4) {
+        // (not with the sorted path: a lane there walks another lane's staged packet)
+        if (p.fast && !p.sort && active_own && (off_own & 15) == 0 && (chunk[0].w & 0xFFFFu) == 0x0008u) {
+            const uint32_t proto = chunk[1].y >> 24;
+            fast = (proto == 17u && len_own >= 42u && (chunk[2].y & 0xFFFFu) != 0xB512u) ||
+                   (proto == 6u && len_own >= 54u);
         }
     }
-    const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
+    // Fast lanes skip the walk; all lanes stage their window and emit from LDS together (one
+    // store per column per wave).  With PKTGPU_FAST_REG a wave whose every packet is fast
+    // decodes from registers instead (wave-uniform branch).
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
+    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
+        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i_own] = (uint8_t)ty;
+        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i_own] = (uint16_t)o;
+    };
+    // fast.rs:5-12 (0x0800 >= 1500) -> parse_ethernet 35-48 (0x0800) -> parse_ipv4 84-98
+    // (17 / 6) -> parse_udp 208-217 (dst != 4789) | parse_tcp 203-207 -> accept 223-227
+    auto fast_result = [&](WalkResult& r) {
+        const bool udp = (chunk[1].y >> 24) == 17u;
+        r.status = PKT_OK;
+        r.n = 3;
+        r.payload_off = udp ? 42u : 54u;
+        r.mask = (1u << PKT_HDR_ETHER) | (1u << PKT_HDR_IPV4) | (udp ? 1u << PKT_HDR_UDP : 1u << PKT_HDR_TCP);
+        r.f_eth = 0;
+        r.f_vlan = -1;
+        r.f_ipv4 = 14;
+        r.f_ipv6 = -1;
+        r.f_tcp = udp ? -1 : 34;
+        r.f_udp = udp ? 34 : -1;
+        push(0, PKT_HDR_ETHER, 0);
+        push(1, PKT_HDR_IPV4, 14);
+        push(2, udp ? PKT_HDR_UDP : PKT_HDR_TCP, 34);
+    };
+    if constexpr (NCH >= 4) {
+        if (PKTGPU_FAST_REG && !p.sort && __ballot(fast) == __ballot(active_own)) {
+            if (!active_own) return;
+            RegView<NCH> rv;
+#pragma unroll
+            for (int c = 0; c < NCH; c++) {
+                rv.w[4 * c] = chunk[c].x;
+                rv.w[4 * c + 1] = chunk[c].y;
+                rv.w[4 * c + 2] = chunk[c].z;
+                rv.w[4 * c + 3] = chunk[c].w;
+            }
+            WalkResult r;
+            fast_result(r);
+            emit_chain<GM>(out, i_own, len_own, r);
+            emit_fields<GM>(out, i_own, rv, r, true);
+            return;
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+#if PKTGPU_LDS_PACKED
+        uint32_t* w = reinterpret_cast<uint32_t*>(lds + t * lane_stride(NCH)) + 4 * c;
+        w[0] = chunk[c].x;
+        w[1] = chunk[c].y;
+        w[2] = chunk[c].z;
+        w[3] = chunk[c].w;
+#else
+        *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
+#endif
+    }
+    const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
 
     if (!p.sort) {
         // ---- unsorted: each lane walks and emits its own packet (no barrier: own LDS only)
         __builtin_amdgcn_wave_barrier();
-        auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
-            if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i_own] = (uint8_t)ty;
-            if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i_own] = (uint16_t)o;
-        };
         WalkResult r;
-        walk(pv_own, entry_state(p.entry), active_own, push, r);
+        walk(pv_own, entry_state(p.entry), active_own && !fast, push, r);
         if (!active_own) return;
+        if constexpr (NCH >= 4) {
+            if (fast) fast_result(r);
+        }
         emit_chain<GM>(out, i_own, len_own, r);
         emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
         return;
@@ -643,6 +722,28 @@ void group_masks(const pkt_out_t& o, uint32_t& full, uint32_t& any) {
 template <class T>
 T* adv(T* p, uint64_t k) { return p ? p + k : p; }
 
+// Element size of each pkt_out_t column, in declaration order (slot columns: one slot).
+constexpr uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
+                               1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
+                               1, 1, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kColHdrType = 2, kColHdrOff = 3;  // slot-major [PKT_MAX_HDRS][n]
+
+// Grow one device buffer of every pipeline slot to `need` bytes (all slots idle: the caller has
+// synchronised the pipeline streams).
+template <class T>
+hipError_t grow(T* (&buf)[HostPipe::kSlots], uint64_t& cap, uint64_t need) {
+    if (need <= cap) return hipSuccess;
+    for (int k = 0; k < HostPipe::kSlots; k++) {
+        if (buf[k]) (void)hipFree(buf[k]);
+        buf[k] = nullptr;
+        hipError_t e = hipMalloc(reinterpret_cast<void**>(&buf[k]), need);
+        if (e != hipSuccess) { cap = 0; return e; }
+    }
+    cap = need;
+    return hipSuccess;
+}
+
+
 }  // namespace
 
 extern "C" {
@@ -657,11 +758,23 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
     c->device = device;
     c->window = 0;
     c->sort = 0;
+    c->fast = 1;
     *out = c;
     return PKT_SUCCESS;
 }
 
 int pkt_ctx_destroy(pkt_ctx_t* ctx) {
+    if (ctx && ctx->hp.init) {
+        (void)hipSetDevice(ctx->device);
+        for (int k = 0; k < HostPipe::kSlots; k++) {
+            (void)hipStreamSynchronize(ctx->hp.s[k]);
+            (void)hipStreamDestroy(ctx->hp.s[k]);
+            (void)hipFree(ctx->hp.slab[k]);
+            (void)hipFree(ctx->hp.offs[k]);
+            (void)hipFree(ctx->hp.lens[k]);
+            (void)hipFree(ctx->hp.out[k]);
+        }
+    }
     delete ctx;
     return PKT_SUCCESS;
 }
@@ -674,14 +787,30 @@ int pkt_ctx_set_window(pkt_ctx_t* ctx, uint32_t w) {
     return PKT_SUCCESS;
 }
 
+int pkt_ctx_set_fastpath(pkt_ctx_t* ctx, int enable) {
+    if (!ctx || enable < 0 || enable > 1) return PKT_ERR_INVALID_ARG;
+    ctx->fast = enable;
+    return PKT_SUCCESS;
+}
+
 int pkt_ctx_set_sort(pkt_ctx_t* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
     ctx->sort = mode;
     return PKT_SUCCESS;
 }
 
+static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
+                      void* stream, uint64_t off_bias);
+
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
+    // the kernel reads whole 16-byte chunks, clamped to the last one of the slab
+    if (b && b->n && b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
+    return parse_impl(ctx, b, entry, out, stream, 0);
+}
+
+static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
+                      void* stream, uint64_t off_bias) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -691,7 +820,7 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
     if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
     if (out->ipv6_src && ((uintptr_t)out->ipv6_src & 15)) return fail(ctx, PKT_ERR_INVALID_ARG, "ipv6_src not 16-byte aligned");
     if (out->ipv6_dst && ((uintptr_t)out->ipv6_dst & 15)) return fail(ctx, PKT_ERR_INVALID_ARG, "ipv6_dst not 16-byte aligned");
-    if (b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
+    if (b->slab_len == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len 0");
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
 
@@ -717,6 +846,7 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
         kp.slab_len = b->slab_len;
         kp.offsets = adv(b->offsets, i0);
         kp.lens = adv(b->lens, i0);
+        kp.off_bias = off_bias;
         kp.i0 = i0;
         kp.n_slot_stride = b->n;
         kp.stride = b->stride;
@@ -724,11 +854,9 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
         kp.entry = entry;
         // auto = off: the sorted path measured slower on C3 and C4
         kp.sort = ctx->sort == 1;
+        kp.fast = ctx->fast && (entry == PKT_ENTRY_PARSE || entry == PKT_ENTRY_ETHERNET);
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
-        static const uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
-                                          1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
-                                          1, 1, 2, 2, 2, 2, 2, 2, 2};
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kSize[c];
         kp.out = o;
@@ -742,6 +870,136 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;
+}
+
+int pkt_host_alloc(pkt_ctx_t* ctx, uint64_t bytes, void** p) {
+    if (!ctx || !p) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    *p = nullptr;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = hipHostMalloc(p, bytes ? bytes : 1, hipHostMallocDefault);
+    return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipHostMalloc");
+}
+
+int pkt_host_free(pkt_ctx_t* ctx, void* p) {
+    if (!p) return PKT_SUCCESS;
+    hipError_t e = hipHostFree(p);
+    return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipHostFree");
+}
+
+int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, uint64_t chunk) {
+    if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    if (b->n == 0) return PKT_SUCCESS;
+    if (!b->slab || b->slab_len == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "null or empty slab");
+    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
+    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    HostPipe& hp = ctx->hp;
+    if (!hp.init) {
+        for (int k = 0; k < HostPipe::kSlots; k++) {
+            e = hipStreamCreateWithFlags(&hp.s[k], hipStreamNonBlocking);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamCreate");
+        }
+        hp.init = true;
+    }
+    const uint64_t n = b->n;
+    const uint64_t cn = std::min<uint64_t>(chunk ? chunk : (1ull << 18), n);
+    const uint64_t nchunks = (n + cn - 1) / cn;
+
+    // bytes of input each chunk needs on the device (indexed: the span its records cover,
+    // from the 16-byte-aligned start of the first)
+    auto span = [&](uint64_t lo, uint64_t hi, uint64_t& base, uint64_t& bytes) {
+        uint64_t a = UINT64_MAX, z = 0;
+        if (b->offsets) {
+            for (uint64_t i = lo; i < hi; i++) {
+                a = std::min(a, b->offsets[i]);
+                z = std::max(z, b->offsets[i] + b->lens[i]);
+            }
+        } else {
+            a = lo * (uint64_t)b->stride;
+            z = hi * (uint64_t)b->stride;
+        }
+        a = std::min(a, b->slab_len);
+        if (b->offsets) a &= ~(uint64_t)15;  // fixed stride: the chunk starts at its first packet
+        z = std::min(z, b->slab_len);
+        base = a;
+        bytes = z > a ? z - a : 0;
+    };
+    uint64_t slab_need = 16;
+    for (uint64_t k = 0; k < nchunks; k++) {
+        uint64_t base, bytes;
+        span(k * cn, std::min(n, (k + 1) * cn), base, bytes);
+        slab_need = std::max(slab_need, bytes);
+    }
+    // device output layout of one chunk: the requested columns, packed, 256-byte aligned
+    const uint8_t* const* hcol = reinterpret_cast<const uint8_t* const*>(out);
+    uint64_t col_off[49], out_need = 0;
+    for (int c = 0; c < 49; c++) {
+        col_off[c] = out_need;
+        if (!hcol[c]) continue;
+        const uint64_t rows = (c == kColHdrType || c == kColHdrOff) ? PKT_MAX_HDRS : 1;
+        out_need += (rows * cn * kSize[c] + 255) & ~(uint64_t)255;
+    }
+    for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
+    if ((e = grow(hp.slab, hp.slab_cap, (slab_need + 15) & ~(uint64_t)15)) != hipSuccess ||
+        (e = grow(hp.out, hp.out_cap, std::max<uint64_t>(out_need, 256))) != hipSuccess)
+        return hip_fail(ctx, e, "hipMalloc (host pipeline)");
+    if (b->offsets || b->lens) {
+        uint64_t cap8 = hp.pkt_cap, cap4 = hp.pkt_cap;
+        if ((e = grow(hp.offs, cap8, cn * 8)) != hipSuccess || (e = grow(hp.lens, cap4, cn * 8)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMalloc (host pipeline)");
+        hp.pkt_cap = std::min(cap8, cap4);
+    }
+
+    int rc = PKT_SUCCESS;
+    for (uint64_t k = 0; k < nchunks && rc == PKT_SUCCESS; k++) {
+        const int q = (int)(k % HostPipe::kSlots);
+        hipStream_t s = hp.s[q];
+        const uint64_t lo = k * cn, hi = std::min(n, lo + cn), m = hi - lo;
+        uint64_t base, bytes;
+        span(lo, hi, base, bytes);
+        // in: the chunk's bytes (+ offsets / lens)
+        if (bytes) e = hipMemcpyAsync(hp.slab[q], b->slab + base, bytes, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && b->offsets)
+            e = hipMemcpyAsync(hp.offs[q], b->offsets + lo, m * 8, hipMemcpyHostToDevice, s);
+        if (e == hipSuccess && b->lens)
+            e = hipMemcpyAsync(hp.lens[q], b->lens + lo, m * 4, hipMemcpyHostToDevice, s);
+        if (e != hipSuccess) { rc = hip_fail(ctx, e, "hipMemcpyAsync H2D"); break; }
+        // parse: a chunk whose records cover no byte still parses (all TRUNCATED) against a
+        // 1-byte view; fixed-stride chunks index from the chunk's first packet
+        pkt_batch_t db;
+        db.slab = hp.slab[q];
+        db.slab_len = std::max<uint64_t>(bytes, 1);
+        db.offsets = b->offsets ? hp.offs[q] : nullptr;
+        db.lens = b->lens ? hp.lens[q] : nullptr;
+        db.stride = b->stride;
+        db.reserved = 0;
+        db.n = m;
+        pkt_out_t dout;
+        uint8_t** dcol = reinterpret_cast<uint8_t**>(&dout);
+        for (int c = 0; c < 49; c++) dcol[c] = hcol[c] ? hp.out[q] + col_off[c] : nullptr;
+        // (the device buffer always has >= 16 readable bytes, so a view shorter than 16 is safe)
+        rc = parse_impl(ctx, &db, entry, &dout, s, b->offsets ? base : 0);
+        if (rc != PKT_SUCCESS) break;
+        // out: every requested column into its host rows [lo, hi)
+        for (int c = 0; c < 49 && e == hipSuccess; c++) {
+            if (!hcol[c]) continue;
+            uint8_t* h = const_cast<uint8_t*>(hcol[c]);
+            const uint64_t sz = kSize[c];
+            if (c == kColHdrType || c == kColHdrOff)
+                e = hipMemcpy2DAsync(h + lo * sz, n * sz, dcol[c], m * sz, m * sz, PKT_MAX_HDRS,
+                                     hipMemcpyDeviceToHost, s);
+            else
+                e = hipMemcpyAsync(h + lo * sz, dcol[c], m * sz, hipMemcpyDeviceToHost, s);
+        }
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMemcpyAsync D2H");
+    }
+    for (int k = 0; k < HostPipe::kSlots; k++) {
+        hipError_t es = hipStreamSynchronize(hp.s[k]);
+        if (es != hipSuccess && rc == PKT_SUCCESS) rc = hip_fail(ctx, es, "hipStreamSynchronize");
+    }
+    return rc;
 }
 
 int pkt_extract_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,

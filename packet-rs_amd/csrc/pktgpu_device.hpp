@@ -1,13 +1,13 @@
 // pktgpu_device.hpp — device code of the batched parser (gfx950 / CDNA4).
 //
-// One lane per packet.  A wave owns a tile of 64 packets and an LDS "window" region laid out
-// chunk-major: chunk c (16 bytes) of lane l lives at win + c*1024 + l*16.  That layout is what
-// one `global_load_lds_dwordx4` wave-instruction writes (wave-uniform base + lane*16), so each
-// wave stages its 64 packets' first W bytes with W/16 (+1 when packet starts are not 16-byte
-// aligned) LDS-DMA loads, each lane gathering its own packet's chunk c.  A lane then walks its
-// packet's header chain out of LDS with dword reads at per-lane byte offsets (v_alignbyte for
-// the unaligned part, v_perm for the big-endian swap); a chain that runs past the window falls
-// back to byte loads from global memory.  Waves never share LDS, so there is no barrier.
+// One lane per packet, 256-packet blocks.  Each lane loads its packet's first NCH 16-byte chunks
+// with per-lane dwordx4 loads.  Aligned Ether/IPv4/UDP|TCP packets are decoded straight from
+// those registers (RegView, the fast path).  Every other packet's chunks are written to the
+// lane's own LDS window (packet-major, odd dword stride: conflict-free per-lane dword reads) and
+// the lane walks its header chain out of LDS with dword reads at per-lane byte offsets
+// (v_alignbyte for the unaligned part, v_perm for the big-endian swap); a chain that runs past
+// the window falls back to dword loads from global memory.  A lane reads only the LDS it wrote,
+// so there is no barrier.
 //
 // The walk is the forward, iterative form of the reference's recursion
 // (src/parser/fast.rs:5-227): each step checks the bounds the reference's slice indexing would
@@ -52,12 +52,14 @@ struct KParams {
     uint64_t slab_len;
     const uint64_t* offsets;
     const uint32_t* lens;
+    uint64_t off_bias;  // subtracted from every offsets[i] (host path: chunk span copied alone)
     uint64_t i0;
     uint64_t n_slot_stride;
     uint32_t stride;
     uint32_t n;
     int entry;
     int sort;  // in-block counting sort by chain class before the walk
+    int fast;  // register fast path for Ether/IPv4/UDP|TCP (entries PARSE / ETHERNET)
     pkt_out_t out;
 };
 
@@ -164,6 +166,21 @@ struct PacketView {
 struct WalkResult {
     uint32_t status, n, payload_off, mask;
     int32_t f_eth, f_vlan, f_ipv4, f_ipv6, f_tcp, f_udp;  // first offsets, -1 = absent
+};
+
+// The first 16*NW bytes of a packet that starts 16-byte aligned, held in registers (little-endian
+// dwords, as loaded).  Same hdr<> interface as PacketView; with a compile-time offset b every
+// index is static, so nothing touches LDS or scratch.
+template <int NW>
+struct RegView {
+    uint32_t w[NW * 4];
+    template <int N>
+    __device__ __forceinline__ void hdr(uint32_t b, uint32_t nbytes, uint32_t (&d)[N]) const {
+        (void)nbytes;
+        const uint32_t k = b >> 2, sh = b & 3u;
+#pragma unroll
+        for (int i = 0; i < N; i++) d[i] = bswap32(__builtin_amdgcn_alignbyte(w[k + i + 1], w[k + i], sh));
+    }
 };
 
 // Header type and size recorded by the walk state S (make_header! sizes, headers.rs:529-827).

@@ -81,6 +81,9 @@ class Parser:
             self._L.pkt_ctx_set_window(self._ctx, window)
 
     def close(self):
+        for p in getattr(self, "_pinned", []):
+            self._L.pkt_host_free(self._ctx, p)
+        self._pinned = []
         if getattr(self, "_ctx", None):
             self._L.pkt_ctx_destroy(self._ctx)
             self._ctx = None
@@ -93,6 +96,10 @@ class Parser:
 
     def set_window(self, window_bytes):
         self._L.pkt_ctx_set_window(self._ctx, int(window_bytes))
+
+    def set_fastpath(self, enable):
+        """Walk-free fast path for aligned Ether/IPv4/UDP|TCP packets (pkt_ctx_set_fastpath)."""
+        self._check(self._L.pkt_ctx_set_fastpath(self._ctx, int(bool(enable))), "pkt_ctx_set_fastpath")
 
     def set_sort(self, mode):
         """0 = auto (indexed batches), 1 = always, 2 = never (see pkt_ctx_set_sort)."""
@@ -155,6 +162,53 @@ class Parser:
         self._check(self._L.pkt_parse_batch(self._ctx, ctypes.byref(b), e, ctypes.byref(o),
                                             self._stream(stream)), "pkt_parse_batch")
         return res
+
+    def parse_host(self, slab, stride=None, n=None, offsets=None, lens=None, entry="parse",
+                   columns="all", out=None, chunk=0):
+        """The host-memory path (pkt_parse_host): numpy slab/offsets/lens in host memory ->
+        {column: numpy array} in host memory, pipelined through the device in chunks.
+        `out` may hold preallocated (e.g. pinned, see host_empty) numpy columns."""
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        slab = np.ascontiguousarray(slab, np.uint8).reshape(-1)
+        b = self._lib.PktBatch()
+        b.slab = slab.ctypes.data
+        b.slab_len = slab.size
+        keep = [slab]
+        if offsets is not None:
+            offsets = np.ascontiguousarray(offsets, np.uint64)
+            lens = np.ascontiguousarray(lens, np.uint32)
+            keep += [offsets, lens]
+            b.offsets, b.lens = offsets.ctypes.data, lens.ctypes.data
+            n = offsets.size if n is None else n
+        else:
+            if lens is not None:
+                lens = np.ascontiguousarray(lens, np.uint32)
+                keep.append(lens)
+                b.lens = lens.ctypes.data
+            n = slab.size // stride if n is None else n
+        b.stride = stride or 0
+        b.n = int(n)
+        if out is None:
+            out = {c: np.zeros(schema.column_shape(c, b.n), schema.column_dtype(c))
+                   for c in resolve_columns(columns)}
+        o = self._lib.PktOut()
+        for c, a in out.items():
+            setattr(o, c, a.ctypes.data if a.size else None)
+        self._check(self._L.pkt_parse_host(self._ctx, ctypes.byref(b), e, ctypes.byref(o), int(chunk)),
+                    "pkt_parse_host")
+        return out
+
+    def host_empty(self, shape, dtype):
+        """A numpy array in pinned host memory (pkt_host_alloc), freed with the Parser."""
+        dtype = np.dtype(dtype)
+        nbytes = int(np.prod(shape)) * dtype.itemsize
+        p = ctypes.c_void_p()
+        self._check(self._L.pkt_host_alloc(self._ctx, max(1, nbytes), ctypes.byref(p)), "pkt_host_alloc")
+        if not hasattr(self, "_pinned"):
+            self._pinned = []
+        self._pinned.append(p)
+        buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
 
     def launch(self, batch_struct, entry, out_struct, stream=None):
         """Relaunch with prebuilt ctypes structs (no per-call Python allocation; bench loop)."""

@@ -56,8 +56,13 @@ SIGNATURES = {
     "pkt_ctx_last_error": (ctypes.c_char_p, [_P]),
     "pkt_ctx_set_window": (ctypes.c_int, [_P, ctypes.c_uint32]),
     "pkt_ctx_set_sort": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pkt_ctx_set_fastpath": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
+    "pkt_parse_host": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.POINTER(PktOut),
+                                      ctypes.c_uint64]),
+    "pkt_host_alloc": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
+    "pkt_host_free": (ctypes.c_int, [_P, _P]),
     "pkt_extract_fields": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
                                           ctypes.POINTER(PktFieldSpec), ctypes.c_uint32,
                                           ctypes.POINTER(_P), ctypes.POINTER(_P), _P]),

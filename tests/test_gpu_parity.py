@@ -388,3 +388,55 @@ def test_sort_modes_bit_exact(P, mode):
                  label=f"mix {entry} s{mode}")
     finally:
         P.set_sort(0)
+
+
+# ------------------------------------------------------------------ register fast path
+def _fastpath_mix(n, stride, seed):
+    """C2-shaped packets with the fields the fast-path classifier reads mutated (EtherType,
+    IP protocol, UDP dst incl. 4789) and lengths clustered around the UDP (42) and TCP (54)
+    header ends, so waves mix fast and walked lanes and every boundary is crossed."""
+    rng = np.random.default_rng(seed)
+    a = gen.gen_c2(n, seed=seed, stride=stride)
+    tcp = rng.random(n) < 0.35
+    a[tcp, 23] = 6
+    r = rng.random(n)
+    a[r < 0.04, 12:14] = [0x86, 0xDD]
+    a[(r >= 0.04) & (r < 0.08), 12:14] = [0x81, 0x00]
+    a[(r >= 0.08) & (r < 0.10), 12:14] = [0x08, 0x01]
+    a[(r >= 0.10) & (r < 0.12), 12:14] = [0x05, 0xDB]  # < 1500: Dot3
+    p = rng.random(n)
+    a[p < 0.03, 23] = rng.choice([1, 4, 41, 47, 58, 0x11, 0x06], int((p < 0.03).sum()))
+    a[(p >= 0.03) & (p < 0.06), 36:38] = [0x12, 0xB5]  # VXLAN port
+    lens = np.where(rng.random(n) < 0.5, rng.integers(36, 60, n), rng.integers(0, stride + 1, n))
+    return a, lens.astype(np.uint32)
+
+
+@pytest.mark.parametrize("fast", [1, 0])
+def test_fastpath_classifier_boundaries(P, fast):
+    """Fixed stride with per-packet lengths: fast path on and off both equal the oracle."""
+    P.set_fastpath(fast)
+    try:
+        for stride in (64, 80, 128):
+            n = 40003
+            a, lens = _fastpath_mix(n, stride, seed=stride + fast)
+            for entry in ("parse", "parse_ethernet", "parse_ipv4"):
+                both(P, a, n, stride=stride, lens=lens, entry=entry, label=f"s{stride} {entry} f{fast}")
+            both(P, a, n, stride=stride, label=f"s{stride} full f{fast}")
+            # aligned indexed batch (offsets multiples of 16) and a misaligned one
+            offs = (np.arange(n, dtype=np.uint64) * stride)
+            both(P, a, n, offsets=offs, lens=lens, label=f"idx s{stride} f{fast}")
+            both(P, np.concatenate([np.zeros(8, np.uint8), a.reshape(-1), np.zeros(8, np.uint8)]), n,
+                 offsets=offs + 8, lens=lens, label=f"idx+8 s{stride} f{fast}")
+    finally:
+        P.set_fastpath(1)
+
+
+def test_fastpath_windows_and_columns(P):
+    """Narrow windows (no fast path below 64 B) and every column subset agree with the oracle."""
+    n = 20000
+    a, lens = _fastpath_mix(n, 64, seed=77)
+    for w in (16, 32, 48, 64):
+        both(P, a, n, stride=64, lens=lens, window=w, label=f"w{w}")
+    for cols in (["status"], ["chain"], ["ether"], ["ipv4"], ["udp"], ["tcp"], ["chain", "udp", "tcp"],
+                 ["ipv4_csum_calc", "udp_dst", "hdr_off", "n_hdrs"]):
+        both(P, a, n, stride=64, lens=lens, columns=cols, label=f"cols {cols}")
