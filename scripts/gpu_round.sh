@@ -13,7 +13,7 @@ echo "== build check"
 ls -la packet-rs_amd/lib oracle/build > "$OUT/ls.txt" 2>&1
 
 echo "== pytest -m gpu"
-timeout -k 10 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > "$OUT/gpu_tests.log" 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -5 "$OUT/gpu_tests.log"
 if crashed $rc; then echo "pytest crashed ($rc), stopping"; exit $rc; fi
 
