@@ -48,6 +48,10 @@ def parse_args():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--fastpath", type=int, default=int(os.environ.get("PKTGPU_FASTPATH", "1")),
                     help="register fast path for Ether/IPv4/UDP|TCP (pkt_ctx_set_fastpath)")
+    ap.add_argument("--staging", type=int, default=int(os.environ.get("PKTGPU_STAGING", "0")),
+                    help="pkt_ctx_set_staging: 0 auto, 1 per-lane windows, 2 wave spans")
+    ap.add_argument("--window", type=int, default=int(os.environ.get("PKTGPU_WINDOW", "0")),
+                    help="pkt_ctx_set_window bytes (0 = auto)")
     ap.add_argument("--streams", type=int, default=2,
                     help="consecutive steps are issued round-robin on this many HIP streams")
     return ap.parse_args()
@@ -124,6 +128,8 @@ def main():
     from pktgpu import schema
     P = pktgpu.Parser(gpu)
     P.set_fastpath(args.fastpath)
+    P.set_staging(args.staging)
+    P.set_window(args.window)
     default_cols = {"c2": "chain,ether,ipv4,udp", "c3": "chain,ether,vlan,ipv4,tcp,udp",
                     "c4": "all", "c5": "chain,ether,ipv4,udp"}[args.config]
     if args.columns is None:
@@ -276,6 +282,7 @@ def main():
                          "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}[args.config],
             "packets_per_gpu": n, "entry": "fast::parse", "columns": args.columns,
             "ring_slabs": ring, "ring_bytes": ring * slab_bytes, "parallelism": f"dp{world}",
+            "staging": args.staging, "window": args.window,
         },
         "GB/s": {"algorithmic": round(algo * world * args.steps / elapsed / 1e9, 2),
                  "slab": round(slab_bytes * world * args.steps / elapsed / 1e9, 2),

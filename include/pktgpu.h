@@ -129,8 +129,8 @@ typedef struct pkt_batch {
  * lazy, headers.rs:195-201 — a caller asks only for what it reads).
  *
  * Chain columns = PacketSlice (lib.rs:136-140, packet.rs:714-761):
- *   hdr_type/hdr_off are slot-major: slot j of packet i lives at [j*n + i]; only slots
- *   j < n_hdrs[i] are written.  List order is the reference's `Vec::insert(0, ..)` order,
+ *   hdr_type/hdr_off are slot-major: slot j of packet i lives at [j*n + i]; slots
+ *   j < n_hdrs[i] hold the chain; later slots are not written.  List order is the reference's `Vec::insert(0, ..)` order,
  *   i.e. wire order except GRE options (Q2: GRE, SeqNum, Key, ChksumOffset).
  *   hdr_off is the header's byte offset from the start of the packet (the Slice's
  *   pointer, headers.rs:187-192); payload_off/payload_len = PacketSlice::payload().
@@ -259,6 +259,13 @@ int         pkt_ctx_set_sort(pkt_ctx_t *ctx, int mode);
  * were loaded into, so it skips the walk.  Results are identical to the walk's (the same fast.rs
  * path; the parity tests run with it forced on and off).  0 = off, 1 = on. */
 int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
+
+/* Tuning knob: how packet bytes reach LDS.  0 = automatic (currently 1), 1 = per-lane windows of
+ * pkt_ctx_set_window bytes (deeper headers read through L2), 2 = wave spans: each wave of 64
+ * packets copies the contiguous byte range its packets occupy (up to 16 KiB; else per-lane
+ * windows) into LDS by LDS-DMA and walks every header from there.  Not with the sorted path.
+ * Results are identical in every mode. */
+int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.

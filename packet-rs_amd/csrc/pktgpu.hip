@@ -36,6 +36,7 @@ struct pkt_ctx {
     uint32_t window;  // 0 = auto
     int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
+    int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     std::string err;
 };
 
@@ -205,7 +206,7 @@ __device__ __forceinline__ uint32_t class_key(const PacketView& pv, bool active)
 }
 
 // Dynamic-LDS carve of a parse block (base 16-byte aligned; nothing static in front of it).
-//   [0, (NCH+1)*kChunkRow)   packet windows, chunk-major (chunk c of packet q at c*kChunkRow + q*16)
+//   [0, window_lds(NCH))     packet windows, packet-major (packet q at q * lane_stride(NCH))
 //   sort part (p.sort only): bucket counts, permutation, the walk results of the 256 packets
 struct SortLds {
     uint32_t hist[64];
@@ -219,25 +220,19 @@ struct SortLds {
     int16_t first[6][kBlock];
 };
 
-#if PKTGPU_LDS_PACKED
 // packet-major: packet q's window at q * lane_stride, lane_stride = 4*NCH+1 dwords (odd, so the
-// per-lane dword reads of the walk hit 64 distinct banks); +16 B for the last lane's over-read
+// per-lane dword reads of the walk hit 64 distinct banks); +16 B for the last lane's over-read.
+// (A chunk-major layout with ds_write_b128 staging had 4-way conflicts on the walk's reads: C4
+// 3 % slower, C2/C3 neutral, scripts/ab_bench.sh.)
 __host__ __device__ constexpr uint32_t lane_stride(int nch) { return (uint32_t)(4 * nch + 1) * 4u; }
 __host__ __device__ constexpr size_t window_lds(int nch) {
     return ((size_t)kBlock * lane_stride(nch) + 16 + 15) & ~(size_t)15;
 }
-#else
-__host__ __device__ constexpr size_t window_lds(int nch) { return (size_t)(nch + 1) * kChunkRow; }
-#endif
 
 __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
                                                 uint32_t len, int nch) {
     PacketView pv;
-#if PKTGPU_LDS_PACKED
     pv.lw = lds + q * lane_stride(nch);
-#else
-    pv.lw = lds + q * 16;
-#endif
     pv.slab = p.slab;
     pv.off = off;
     pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
@@ -257,6 +252,70 @@ __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uin
     if (want<GM, G_CHAIN>(out.hdr_mask)) st<uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Lane t's packet range and its first NCH 16-byte chunks (from the 16-byte-aligned start) by
+// per-lane dwordx4 loads (faster than the LDS-DMA gather, scripts/probe.py).  Chunks past the
+// readable end of the slab (round_up(slab_len, 16)) are clamped to an in-bounds chunk; those
+// bytes lie beyond every packet and are never interpreted.
+template <int NCH>
+__device__ __forceinline__ void load_packet(const KParams& p, uint32_t i, bool active, u32x4 (&chunk)[NCH],
+                                            uint64_t& off, uint32_t& len) {
+    off = 0;
+    len = 0;
+    if (active) packet_range(p, i, off, len);
+    const uint64_t a0 = off & ~(uint64_t)15;
+    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        uint64_t o = a0 + 16u * (uint32_t)c;
+        o = o > last16 ? last16 : o;
+#if PKTGPU_NT_LOAD
+        chunk[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p.slab + o));
+#else
+        chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
+#endif
+    }
+}
+
+// Packet q's window: its chunks as dwords at q * lane_stride(NCH) (odd dword stride).
+template <int NCH>
+__device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32x4 (&chunk)[NCH]) {
+#pragma unroll
+    for (int c = 0; c < NCH; c++) {
+        uint32_t* w = reinterpret_cast<uint32_t*>(lds + q * lane_stride(NCH)) + 4 * c;
+        w[0] = chunk[c].x;
+        w[1] = chunk[c].y;
+        w[2] = chunk[c].z;
+        w[3] = chunk[c].w;
+    }
+}
+
+template <int NCH, uint32_t GM>
+__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortLds& S, uint32_t base,
+                                           const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
+                                           bool active_own);
+
+// One block = 256 packets, one lane per packet.  (A persistent grid of k blocks per CU striding
+// over the tiles, each lane's loads of its next packet in flight while it parsed the current one,
+// was measured no faster at k = 4 and slower at k = 1, 2: DESIGN.md §5.)
+#ifndef PKTGPU_WAVES_PER_EU
+#define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
+#endif
+template <int NCH, uint32_t GM>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
+void parse_kernel(KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    SortLds& S = *reinterpret_cast<SortLds*>(lds + window_lds(NCH));  // only touched if p.sort
+    const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
+    const bool act = base + threadIdx.x < p.n;
+    u32x4 chunk[NCH];
+    uint64_t off;
+    uint32_t len;
+    load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
+    parse_tile<NCH, GM>(p, lds, S, base, chunk, off, len, act);
+}
+
 template <int NCH, uint32_t GM>
 #ifndef PKTGPU_FAST_REG
 // 1: waves whose packets all take the fast path decode from registers, no LDS.  0 (default):
@@ -264,42 +323,11 @@ template <int NCH, uint32_t GM>
 // 24.0 us pipelined per step, LDS 29.8 / 23.4 — the pipelined rate is the bench's value.
 #define PKTGPU_FAST_REG 0
 #endif
-#ifndef PKTGPU_WAVES_PER_EU
-#define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
-#endif
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
-void parse_kernel(KParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    SortLds& S = *reinterpret_cast<SortLds*>(lds + window_lds(NCH));  // only touched if p.sort
+__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortLds& S, uint32_t base,
+                                           const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
+                                           bool active_own) {
     const uint32_t t = threadIdx.x;
-    const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
     const uint32_t i_own = base + t;
-    const bool active_own = i_own < p.n;
-    uint64_t off_own = 0;
-    uint32_t len_own = 0;
-    if (active_own) packet_range(p, i_own, off_own, len_own);
-
-    // ---- stage: lane t loads ITS packet's first NCH 16-byte chunks (from the 16-byte-aligned
-    // start) with per-lane dwordx4 loads (faster than the LDS-DMA gather, scripts/probe.py) and
-    // writes them with conflict-free ds_write_b128 (an 8-lane write group spans all banks).
-    // Chunks past the readable end of the slab (round_up(slab_len, 16)) are clamped to an
-    // in-bounds chunk; those bytes lie beyond every packet and are never interpreted.
-    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-    u32x4 chunk[NCH];
-    {
-        const uint64_t a0 = off_own & ~(uint64_t)15;
-        const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
-#pragma unroll
-        for (int c = 0; c < NCH; c++) {
-            uint64_t o = a0 + 16u * (uint32_t)c;
-            o = o > last16 ? last16 : o;
-#if PKTGPU_NT_LOAD
-            chunk[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p.slab + o));
-#else
-            chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
-#endif
-        }
-    }
     // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose bytes 12-13 = 0x0800,
     // byte 23 = 17 with bytes 36-37 != 4789 and len >= 42, or byte 23 = 6 and len >= 54, takes
     // exactly fast.rs's Ether -> IPv4 -> UDP|TCP -> accept path (no bound or depth check can
@@ -358,18 +386,7 @@ void parse_kernel(KParams p) {
             return;
         }
     }
-#pragma unroll
-    for (int c = 0; c < NCH; c++) {
-#if PKTGPU_LDS_PACKED
-        uint32_t* w = reinterpret_cast<uint32_t*>(lds + t * lane_stride(NCH)) + 4 * c;
-        w[0] = chunk[c].x;
-        w[1] = chunk[c].y;
-        w[2] = chunk[c].z;
-        w[3] = chunk[c].w;
-#else
-        *reinterpret_cast<u32x4*>(lds + c * kChunkRow + t * 16) = chunk[c];
-#endif
-    }
+    stage_window<NCH>(lds, t, chunk);
     const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
 
     if (!p.sort) {
@@ -377,10 +394,10 @@ void parse_kernel(KParams p) {
         __builtin_amdgcn_wave_barrier();
         WalkResult r;
         walk(pv_own, entry_state(p.entry), active_own && !fast, push, r);
-        if (!active_own) return;
         if constexpr (NCH >= 4) {
             if (fast) fast_result(r);
         }
+        if (!active_own) return;
         emit_chain<GM>(out, i_own, len_own, r);
         emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
         return;
@@ -459,6 +476,94 @@ void parse_kernel(KParams p) {
     }
     emit_chain<GM>(out, i_own, len_own, r);
     emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+}
+
+// ---- span staging (indexed batches: the records of a pcap lie back to back) ----
+// The 64 records of a wave usually occupy ONE contiguous byte range of the slab.  The wave copies
+// that range [lo & ~15, hi) into its LDS region by LDS-DMA (global_load_lds_dwordx4: 1 KiB of
+// consecutive bytes per wave-instruction, fully coalesced, no VGPRs) and every lane then walks its
+// record entirely out of LDS: no per-lane window, no global-memory reads for deep tunnels, and
+// each HBM line is fetched once.  A wave whose range exceeds the region (records far apart or
+// long) stages per-lane windows into the same region instead (the parse_kernel staging).
+#define LDS_AS __attribute__((address_space(3)))
+#ifndef PKTGPU_SPAN_CAP
+#define PKTGPU_SPAN_CAP 16384u  // bytes of range one wave stages (a multiple of 1024)
+#endif
+static_assert(PKTGPU_SPAN_CAP % 1024u == 0, "span cap: whole 1 KiB LDS-DMA pieces");
+constexpr uint32_t kSpanBlock = 64;  // one wave per block: one LDS region per block
+__host__ __device__ constexpr uint32_t span_region(int nch) {
+    // the range, or the fallback's 64 packed windows; +16: the walk's dword over-read
+    return ((PKTGPU_SPAN_CAP > 64u * lane_stride(nch) ? PKTGPU_SPAN_CAP : 64u * lane_stride(nch)) + 16u + 15u) & ~15u;
+}
+
+__device__ __forceinline__ uint64_t wave_uniform64(uint64_t v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
+template <int NCH, uint32_t GM>
+__global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
+    const bool active = i < p.n;
+    uint64_t off = 0;
+    uint32_t len = 0;
+    if (active) packet_range(p, i, off, len);
+    // the wave's byte range [lo, hi) (butterfly min/max; lane 0 is always active)
+    uint64_t lo = active ? off : ~(uint64_t)0, hi = active ? off + len : 0;
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint64_t l2 = __shfl_xor(lo, m, 64), h2 = __shfl_xor(hi, m, 64);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+    }
+    const uint64_t a0 = wave_uniform64(lo) & ~(uint64_t)15;
+    const uint64_t hi_u = wave_uniform64(hi);
+    const uint64_t bytes = hi_u > a0 ? hi_u - a0 : 0;
+    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+    PacketView pv;
+    if (bytes <= PKTGPU_SPAN_CAP) {  // wave-uniform
+        const uint32_t npiece = (uint32_t)((bytes + 1023) >> 10);
+        for (uint32_t k = 0; k < npiece; k++) {
+            uint64_t o = a0 + ((uint64_t)k << 10) + lane * 16u;
+            o = o > last16 ? last16 : o;  // bytes past the slab end lie beyond every record
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(p.slab + o),
+                                             (LDS_AS void*)(lds + (k << 10)), 16, 0, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const uint32_t rel = active ? (uint32_t)(off - a0) : 0u;
+        pv.lw = lds + (rel & ~3u);
+        pv.slab = p.slab;
+        pv.off = off;
+        pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
+        pv.shift = rel & 3u;
+        pv.win_end = (npiece << 10) - rel;  // >= len: the whole record is in LDS
+        pv.len = len;
+    } else {
+        u32x4 chunk[NCH];
+        const uint64_t c0 = off & ~(uint64_t)15;
+#pragma unroll
+        for (int c = 0; c < NCH; c++) {
+            uint64_t o = c0 + 16u * (uint32_t)c;
+            o = o > last16 ? last16 : o;
+            chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
+        }
+        stage_window<NCH>(lds, lane, chunk);
+        pv = make_view(p, lds, lane, off, len, NCH);
+    }
+    const pkt_out_t& out = p.out;
+    const uint64_t ns = p.n_slot_stride;
+    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
+        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)ty;
+        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
+    };
+    WalkResult r;
+    walk(pv, entry_state(p.entry), active, push, r);
+    if (!active) return;
+    emit_chain<GM>(out, i, len, r);
+    emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
 }
 
 // Batched `<Hdr>Slice::<field>()` (headers.rs:195-201 -> bit_range 252-263).
@@ -679,23 +784,31 @@ int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
     return PKT_ERR_HIP;
 }
 
+// How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
+enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
+
 template <int NCH, uint32_t GM>
-hipError_t launch_parse(const KParams& kp, hipStream_t s) {
-    dim3 grid((unsigned)((kp.n + kBlock - 1) / kBlock));
-    const size_t lds = window_lds(NCH) + (kp.sort ? sizeof(SortLds) : 0);
-    hipLaunchKernelGGL((parse_kernel<NCH, GM>), grid, dim3(kBlock), lds, s, kp);
+hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
+    if (mode == M_SPAN) {
+        hipLaunchKernelGGL((parse_span_kernel<NCH, GM>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
+                           dim3(kSpanBlock), span_region(NCH), s, kp);
+    } else {
+        const size_t lds = window_lds(NCH) + (kp.sort ? sizeof(SortLds) : 0);
+        hipLaunchKernelGGL((parse_kernel<NCH, GM>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
+                           lds, s, kp);
+    }
     return hipGetLastError();
 }
 
 template <int NCH>
-hipError_t launch_gm(const KParams& kp, uint32_t gm, hipStream_t s) {
+hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, hipStream_t s) {
     switch (gm) {
-        case G_CHAIN: return launch_parse<NCH, G_CHAIN>(kp, s);
-        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_parse<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP>(kp, s);
+        case G_CHAIN: return launch_mode<NCH, G_CHAIN>(kp, mode, s);
+        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP>(kp, mode, s);
         case G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP:
-            return launch_parse<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP>(kp, s);
-        case G_ALL: return launch_parse<NCH, G_ALL>(kp, s);
-        default: return launch_parse<NCH, G_RUNTIME>(kp, s);
+            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP>(kp, mode, s);
+        case G_ALL: return launch_mode<NCH, G_ALL>(kp, mode, s);
+        default: return launch_mode<NCH, G_RUNTIME>(kp, mode, s);
     }
 }
 
@@ -759,6 +872,7 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
     c->window = 0;
     c->sort = 0;
     c->fast = 1;
+    c->staging = 0;
     *out = c;
     return PKT_SUCCESS;
 }
@@ -790,6 +904,12 @@ int pkt_ctx_set_window(pkt_ctx_t* ctx, uint32_t w) {
 int pkt_ctx_set_fastpath(pkt_ctx_t* ctx, int enable) {
     if (!ctx || enable < 0 || enable > 1) return PKT_ERR_INVALID_ARG;
     ctx->fast = enable;
+    return PKT_SUCCESS;
+}
+
+int pkt_ctx_set_staging(pkt_ctx_t* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
+    ctx->staging = mode;
     return PKT_SUCCESS;
 }
 
@@ -838,6 +958,9 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     group_masks(*out, full, any);
     const uint32_t gm = (full == any) ? full : G_RUNTIME;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // Staging: wave spans when asked (not with the sorted path); per-lane windows otherwise
+    // (auto: spans measured slower on C3 and C4).
+    const int mode = (ctx->staging == 2 && ctx->sort != 1) ? M_SPAN : M_TILE;
     const uint64_t kChunk = 1ull << 26;  // packets per launch (32-bit byte offsets in-kernel)
     for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kChunk) {
         const uint64_t cnt = std::min<uint64_t>(kChunk, b->n - i0);
@@ -860,13 +983,13 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kSize[c];
         kp.out = o;
-        if (nch <= 2) e = launch_gm<2>(kp, gm, s);
-        else if (nch <= 4) e = launch_gm<4>(kp, gm, s);
-        else if (nch <= 5) e = launch_gm<5>(kp, gm, s);
-        else if (nch <= 8) e = launch_gm<8>(kp, gm, s);
-        else if (nch <= 9) e = launch_gm<9>(kp, gm, s);
-        else if (nch <= 16) e = launch_gm<16>(kp, gm, s);
-        else e = launch_gm<17>(kp, gm, s);
+        if (nch <= 2) e = launch_gm<2>(kp, gm, mode, s);
+        else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, s);
+        else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, s);
+        else if (nch <= 8) e = launch_gm<8>(kp, gm, mode, s);
+        else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, s);
+        else if (nch <= 16) e = launch_gm<16>(kp, gm, mode, s);
+        else e = launch_gm<17>(kp, gm, mode, s);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;

@@ -21,19 +21,11 @@
 
 #include "../../include/pktgpu.h"
 
-// LDS window layout.  1 (default): packet-major, odd lane stride (conflict-free per-lane dword
-// reads; C4 -3 %, C2/C3 neutral, scripts/ab_bench.sh).  0: chunk-major (ds_write_b128 staging,
-// 4-way bank conflicts on the walk's dword reads).
-#ifndef PKTGPU_LDS_PACKED
-#define PKTGPU_LDS_PACKED 1
-#endif
-
 namespace pktgpu {
 
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;
 constexpr int kBlock = kWave * kWavesPerBlock;
-constexpr int kChunkRow = kBlock * 16;  // bytes of one chunk row: chunk c of the block's 256 packets
 
 // Walk states = the parse_* functions of fast.rs (+ accept / done markers).
 enum State : uint32_t {
@@ -98,7 +90,7 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 // A lane's view of its packet: LDS window + global fallback.
 struct PacketView {
-    const uint8_t* lw;        // LDS window of this packet: block window + q*16 (chunk-major)
+    const uint8_t* lw;        // LDS window of this packet (dword-aligned)
     const uint8_t* slab;      // slab base (16-byte aligned)
     uint64_t off;             // packet start in the slab
     uint64_t last4;           // last readable aligned dword offset of the slab
@@ -108,11 +100,7 @@ struct PacketView {
 
     // aligned dword k of the window
     __device__ __forceinline__ uint32_t wdw(uint32_t k) const {
-#if PKTGPU_LDS_PACKED
         return reinterpret_cast<const uint32_t*>(lw)[k];
-#else
-        return *reinterpret_cast<const uint32_t*>(lw + (k >> 2) * kChunkRow + (k & 3) * 4);
-#endif
     }
     // aligned dword of the slab containing slab byte a (clamped to the readable end)
     __device__ __forceinline__ uint32_t gdw(uint64_t a) const {
@@ -309,9 +297,61 @@ __device__ __forceinline__ void step(Lane& L, const PacketView& pv, Push& push) 
 // state of the first live lane (v_readlane), and every live lane in that state advances one
 // step under a SCALAR switch — a wave whose packets share a layout runs exactly one case per
 // header, a mixed wave one case per distinct state.
+// Walk schedule.  0: the waterfall above.  1: sweeps — the states in chain order (L2 -> L3 -> L4 ->
+// tunnel), each run while any lane is in it, repeated until no lane is live: a lane advances
+// through every forward edge of its chain within one sweep, and only the edges back to an earlier
+// state (tunnels to Ethernet/IP, IPv6 -> IPv4) wait for the next sweep.
+#ifndef PKTGPU_WALK_SWEEP
+#define PKTGPU_WALK_SWEEP 0
+#endif
+
+template <uint32_t S, class Push>
+__device__ __forceinline__ void sweep_state(Lane& L, const PacketView& pv, Push& push) {
+    while (__ballot(L.live && L.st == S)) {
+        if (L.live && L.st == S) {
+            if (++L.steps > PKT_MAX_HDRS + 3) fail(L, PKT_DEPTH_LIMIT);
+            else step<S>(L, pv, push);
+        }
+    }
+}
+
 template <class Push>
 __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool active, Push&& push,
                                      WalkResult& out) {
+#if PKTGPU_WALK_SWEEP
+    Lane L;
+    L.st = state;
+    L.o = 0;
+    L.steps = 0;
+    L.live = active;
+    L.r.status = PKT_OK;
+    L.r.n = 0;
+    L.r.payload_off = 0;
+    L.r.mask = 0;
+    L.r.f_eth = L.r.f_vlan = L.r.f_ipv4 = L.r.f_ipv6 = L.r.f_tcp = L.r.f_udp = -1;
+    while (__ballot(L.live)) {
+        sweep_state<S_PARSE>(L, pv, push);
+        sweep_state<S_DOT3>(L, pv, push);
+        sweep_state<S_LLC>(L, pv, push);
+        sweep_state<S_SNAP>(L, pv, push);
+        sweep_state<S_ETHER>(L, pv, push);
+        sweep_state<S_VLAN>(L, pv, push);
+        sweep_state<S_MPLS>(L, pv, push);
+        sweep_state<S_MPLS_BOS>(L, pv, push);
+        sweep_state<S_ARP>(L, pv, push);
+        sweep_state<S_IPV6>(L, pv, push);
+        sweep_state<S_IPV4>(L, pv, push);
+        sweep_state<S_ICMP>(L, pv, push);
+        sweep_state<S_TCP>(L, pv, push);
+        sweep_state<S_UDP>(L, pv, push);
+        sweep_state<S_VXLAN>(L, pv, push);
+        sweep_state<S_GRE>(L, pv, push);
+        sweep_state<S_ERSPAN2>(L, pv, push);
+        sweep_state<S_ERSPAN3>(L, pv, push);
+        sweep_state<S_ACCEPT>(L, pv, push);
+    }
+    out = L.r;
+#else
     Lane L;
     L.st = state;
     L.o = 0;
@@ -361,6 +401,7 @@ __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool 
         }
     }
     out = L.r;
+#endif
 }
 
 }  // namespace pktgpu

@@ -101,6 +101,10 @@ class Parser:
         """Walk-free fast path for aligned Ether/IPv4/UDP|TCP packets (pkt_ctx_set_fastpath)."""
         self._check(self._L.pkt_ctx_set_fastpath(self._ctx, int(bool(enable))), "pkt_ctx_set_fastpath")
 
+    def set_staging(self, mode):
+        """0 = auto, 1 = per-lane windows, 2 = wave spans (pkt_ctx_set_staging)."""
+        self._check(self._L.pkt_ctx_set_staging(self._ctx, int(mode)), "pkt_ctx_set_staging")
+
     def set_sort(self, mode):
         """0 = auto (indexed batches), 1 = always, 2 = never (see pkt_ctx_set_sort)."""
         self._check(self._L.pkt_ctx_set_sort(self._ctx, int(mode)), "pkt_ctx_set_sort")

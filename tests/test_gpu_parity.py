@@ -440,3 +440,56 @@ def test_fastpath_windows_and_columns(P):
     for cols in (["status"], ["chain"], ["ether"], ["ipv4"], ["udp"], ["tcp"], ["chain", "udp", "tcp"],
                  ["ipv4_csum_calc", "udp_dst", "hdr_off", "n_hdrs"]):
         both(P, a, n, stride=64, lens=lens, columns=cols, label=f"cols {cols}")
+
+
+# ------------------------------------------------------------------ launch modes (grid, staging)
+def _mode_cases(P, label):
+    """Every launch mode must agree with the oracle on the same mixes: golden pcap, C4 pcap
+    (indexed, unaligned records), C3/C2 fixed stride, the fast-path mix with per-packet lengths,
+    and random/truncated records back to back."""
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    offs, lens = gen.pcap_index_py(pc)
+    both(P, np.frombuffer(pc, np.uint8), 22, offsets=offs, lens=lens, label=f"ref22 {label}")
+    buf, offs, lens = gen.gen_c4(30011, seed=51)
+    both(P, buf, len(offs), offsets=offs, lens=lens, label=f"c4 {label}")
+    both(P, buf, len(offs), offsets=offs, lens=lens, columns=["chain"], label=f"c4 chain {label}")
+    slab = gen.gen_c3(20011, seed=52)
+    both(P, slab, 20011, stride=128, label=f"c3 {label}")
+    slab = gen.gen_c2(70001, seed=53)
+    both(P, slab, 70001, stride=64, columns=["chain", "ether", "ipv4", "udp"], label=f"c2 {label}")
+    a, ln = _fastpath_mix(20000, 64, seed=54)
+    both(P, a, 20000, stride=64, lens=ln, label=f"fastmix {label}")
+    rng = np.random.default_rng(55)
+    pk = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes() for _ in range(3000)]
+    pk += [p.to_vec()[:int(rng.integers(10, 300))] for p in gen.reference_22_packets() for _ in range(40)]
+    b = b"".join(pk)
+    ln = np.array([len(x) for x in pk], np.uint32)
+    of = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    for entry in ("parse", "parse_ipv4", "parse_gre"):
+        both(P, np.frombuffer(b + bytes(16), np.uint8), len(pk), offsets=of, lens=ln, entry=entry,
+             label=f"mix {entry} {label}")
+    # records out of order and far apart (wave ranges beyond the span region: window fallback)
+    perm = rng.permutation(len(pk))
+    both(P, np.frombuffer(b + bytes(16), np.uint8), len(pk), offsets=of[perm], lens=ln[perm],
+         label=f"shuffled {label}")
+    # one long record per wave (> 16 KiB range) next to short ones
+    big = np.zeros(40000, np.uint8)
+    big[:64] = gen.gen_c2(1, seed=56)[0]
+    of2 = np.array([0, 20000, 39000, 100, 200], np.uint64)
+    ln2 = np.array([40000, 64, 1000, 64, 50], np.uint32)
+    both(P, big, 5, offsets=of2, lens=ln2, label=f"long {label}")
+
+
+@pytest.mark.parametrize("staging", [1, 2])
+def test_staging_modes_bit_exact(P, staging):
+    """Per-lane windows (1) and wave spans (2) give identical columns."""
+    P.set_staging(staging)
+    try:
+        _mode_cases(P, f"st{staging}")
+        for w in (16, 64, 144):
+            P.set_window(w)
+            buf, offs, lens = gen.gen_c4(5003, seed=57 + w)
+            both(P, buf, len(offs), offsets=offs, lens=lens, window=w, label=f"c4 w{w} st{staging}")
+    finally:
+        P.set_staging(0)
+        P.set_window(0)
