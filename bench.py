@@ -87,11 +87,12 @@ def cpu_baseline(slab, stride, offs, lens, n, cols, threads):
     n = min(n, 1 << 20)  # bounded sample (c5 shards are up to 2^24 packets)
     if offs is not None:
         offs, lens = offs[:n], lens[:n]
-    reps = 4
-    t0 = time.perf_counter()
-    for _ in range(reps):
+    # passes over the same slab until ~8 s of wall time (>= 2 passes): a bounded sample
+    reps, t0 = 0, time.perf_counter()
+    while reps < 2 or (time.perf_counter() - t0 < 8.0 and reps < 400):
         oracle.parse_batch(slab, n, stride=stride, offsets=offs, lens=lens, columns=cols,
                            nthreads=threads)
+        reps += 1
     dt = time.perf_counter() - t0
     n1 = min(n, 1 << 19)
     t1 = time.perf_counter()

@@ -279,9 +279,11 @@ int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
  * pkt_out_t layout of pkt_parse_batch with slot columns strided by batch->n) are host memory.
  * The batch is cut into chunks of `chunk` packets (0 = 262144) pipelined over three streams of
  * the ctx: the copy-in of chunk k+1 and the copy-out of chunk k-1 overlap the parse of chunk k.
- * Indexed chunks copy the byte span their records cover.  Host buffers from pkt_host_alloc
- * (pinned) move at link rate; pageable ones work, staged by the runtime.  Blocks until every
- * output is in host memory.  One host call at a time per ctx. */
+ * Indexed chunks copy the byte span their records cover.  When the slab, offsets, lens and every
+ * requested column are pinned memory from pkt_host_alloc, there are no copies at all: one launch
+ * reads the slab and writes the columns over the link directly (zero copy; `chunk` unused).
+ * Pageable buffers work, staged by the runtime.  Blocks until every output is in host memory.
+ * One host call at a time per ctx. */
 int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pkt_out_t *out,
                    uint64_t chunk);
 /* Pinned (page-locked) host memory for pkt_parse_host buffers. */

@@ -835,6 +835,26 @@ void group_masks(const pkt_out_t& o, uint32_t& full, uint32_t& any) {
 template <class T>
 T* adv(T* p, uint64_t k) { return p ? p + k : p; }
 
+// Is `p` pinned host memory the device can address?  On success `dev` = its device address.
+template <class T>
+bool host_mapped(const T* p, const T*& dev) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();  // pageable memory: not an error for the caller
+        return false;
+    }
+    if (a.type != hipMemoryTypeHost || !a.devicePointer) return false;
+    dev = reinterpret_cast<const T*>(a.devicePointer);
+    return true;
+}
+template <class T>
+bool host_mapped(T* p, T*& dev) {
+    const T* d = nullptr;
+    if (!host_mapped<T>(static_cast<const T*>(p), d)) return false;
+    dev = const_cast<T*>(d);
+    return true;
+}
+
 // Element size of each pkt_out_t column, in declaration order (slot columns: one slot).
 constexpr uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
                                1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
@@ -1025,6 +1045,29 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
             if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamCreate");
         }
         hp.init = true;
+    }
+    // Zero copy: when the slab, the index arrays and every requested column are pinned host memory
+    // mapped into the device (pkt_host_alloc), the kernel reads and writes them over PCIe directly —
+    // one launch, no staging copies, both link directions busy at once.
+    {
+        pkt_batch_t db = *b;
+        pkt_out_t dout = *out;
+        bool mapped = host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
+                      (!b->lens || host_mapped(b->lens, db.lens));
+        uint8_t** dc = reinterpret_cast<uint8_t**>(&dout);
+        for (int c = 0; c < 49 && mapped; c++)
+            if (dc[c]) mapped = host_mapped(dc[c], dc[c]);
+        if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
+            // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
+            // for a deep header (per-lane windows would, one dependent PCIe read each)
+            const int st = ctx->staging;
+            if (st == 0) ctx->staging = 2;
+            int rc = parse_impl(ctx, &db, entry, &dout, hp.s[0], 0);
+            ctx->staging = st;
+            if (rc != PKT_SUCCESS) return rc;
+            e = hipStreamSynchronize(hp.s[0]);
+            return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipStreamSynchronize");
+        }
     }
     const uint64_t n = b->n;
     const uint64_t cn = std::min<uint64_t>(chunk ? chunk : (1ull << 18), n);

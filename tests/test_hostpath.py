@@ -88,3 +88,22 @@ def test_pinned_buffers(P):
         out[c][...] = 0
     g = P.parse_host(slab, stride=64, columns=cols, out=out, chunk=1 << 15)
     check(g, oracle.parse_batch(src, n, stride=64, columns=cols, nthreads=8), "pinned")
+
+
+def test_pinned_indexed_zero_copy(P):
+    """Pinned slab, offsets, lens and columns: the zero-copy route (one launch over the link)."""
+    buf, offs, lens = gen.gen_c4(40000, seed=11)
+    h = P.host_empty(buf.shape, np.uint8)
+    h[:] = buf
+    ho = P.host_empty(offs.shape, np.uint64)
+    ho[:] = offs
+    hl = P.host_empty(lens.shape, np.uint32)
+    hl[:] = lens
+    out = {c: P.host_empty(schema.column_shape(c, len(offs)), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
+    for c in out:
+        out[c][...] = 0
+    g = P.parse_host(h, offsets=ho, lens=hl, out=out)
+    check(g, oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8), "pinned c4")
+    # mixed: pinned slab, pageable columns -> the staged pipeline, same results
+    g = P.parse_host(h, offsets=ho, lens=hl, columns="all", chunk=9999)
+    check(g, oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8), "pinned slab only")
