@@ -54,6 +54,35 @@ __global__ __launch_bounds__(256) void k_store(const uint8_t* slab, uint32_t n, 
     }
 }
 
+// R packets per lane, packet g + r*(n/R) for r < R (all R loads issued first), each stored with
+// the K=1 shape: a lane runs R rounds of the same per-packet stores, so the grid has 1/R the waves.
+template <int R>
+__global__ __launch_bounds__(256) void k_rounds(const uint8_t* slab, uint32_t n, Cols c) {
+    const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t part = n / R;
+    if (g >= part) return;
+    uint4 q[R][4];
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint4* p = (const uint4*)(slab + (uint64_t)(g + r * part) * 64);
+        q[r][0] = p[0]; q[r][1] = p[1]; q[r][2] = p[2]; q[r][3] = p[3];
+    }
+#pragma unroll
+    for (int r = 0; r < R; r++) {
+        const uint32_t i = g + r * part;
+        uint4 a = q[r][0], b = q[r][1], cc = q[r][2], d = q[r][3];
+        uint32_t v[8] = {a.x, a.y ^ b.x, a.z ^ b.y, a.w ^ b.z, cc.x ^ b.w, cc.y ^ d.x, cc.z ^ d.y, cc.w ^ d.z};
+#pragma unroll
+        for (int k = 0; k < 11; k++) ((uint8_t*)c.p[k])[i] = (uint8_t)(v[k & 7] >> k);
+#pragma unroll
+        for (int k = 11; k < 26; k++) ((uint16_t*)c.p[k])[i] = (uint16_t)(v[k & 7] >> (k & 15));
+#pragma unroll
+        for (int k = 26; k < 29; k++) ((uint32_t*)c.p[k])[i] = v[k & 7] + k;
+#pragma unroll
+        for (int k = 29; k < 31; k++) ((uint64_t*)c.p[k])[i] = ((uint64_t)v[k & 7] << 16) ^ v[(k + 1) & 7];
+    }
+}
+
 // ideal store shape: chunk q of packet i at out[q][i] (16 B), q = 0..3, plus one u64 column
 __global__ __launch_bounds__(256) void k_ideal(const uint8_t* slab, uint32_t n, Cols c) {
     const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -76,6 +105,8 @@ extern "C" int probe_store(int which, const uint8_t* slab, uint32_t n, void* con
         case 1: hipLaunchKernelGGL(k_store<2>, dim3((n / 2 + 255) / 256), dim3(256), 0, s, slab, n, c); break;
         case 2: hipLaunchKernelGGL(k_store<4>, dim3((n / 4 + 255) / 256), dim3(256), 0, s, slab, n, c); break;
         case 3: hipLaunchKernelGGL(k_ideal, dim3((n + 255) / 256), dim3(256), 0, s, slab, n, c); break;
+        case 4: hipLaunchKernelGGL(k_rounds<2>, dim3((n / 2 + 255) / 256), dim3(256), 0, s, slab, n, c); break;
+        case 5: hipLaunchKernelGGL(k_rounds<4>, dim3((n / 4 + 255) / 256), dim3(256), 0, s, slab, n, c); break;
         default: return -1;
     }
     return hipGetLastError() == hipSuccess ? 0 : -2;

@@ -31,7 +31,8 @@ for nm, sz in (("tuple", sizes), ("ideal", ideal)):
         sets[nm].append((cols, (ctypes.c_void_p * 31)(*[c.data_ptr() for c in cols])))
 st = torch.cuda.current_stream()
 variants = [("K=1 (per-lane narrow stores)", 0, "tuple", 133), ("K=2", 1, "tuple", 133),
-            ("K=4", 2, "tuple", 133), ("ideal 72 B (uint4 columns)", 3, "ideal", 136)]
+            ("K=4", 2, "tuple", 133), ("ideal 72 B (uint4 columns)", 3, "ideal", 136),
+            ("2 packets/lane, K=1 stores", 4, "tuple", 133), ("4 packets/lane, K=1 stores", 5, "tuple", 133)]
 R = 50
 res = {v[0]: [] for v in variants}
 for k in range(2 * ring):
@@ -51,3 +52,22 @@ for rnd in range(5):
 for nm, w, cs, bpp in variants:
     us = float(np.median(res[nm]))
     print(f"{nm:32s} {us:8.2f} us/launch  {n * bpp / us / 1e3:8.1f} GB/s ({bpp} B/pkt)", flush=True)
+
+# pipelined: launches round-robin on 2 streams (as bench.py's timed region), device time per launch
+streams = [torch.cuda.Stream() for _ in range(2)]
+for nm, w, cs, bpp in variants[:1] + variants[4:]:
+    ts = []
+    for rnd in range(5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s0 = streams[0]
+        a.record(s0)
+        streams[1].wait_stream(s0)
+        for k in range(200):
+            s_ = streams[k % 2]
+            L.probe_store(w, slabs[k % ring].data_ptr(), n, sets[cs][k % ring][1], ctypes.c_void_p(s_.cuda_stream))
+        s0.wait_stream(streams[1])
+        b.record(s0)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3 / 200)
+    us = float(np.median(ts))
+    print(f"pipelined 2 streams {nm:22s} {us:8.2f} us/launch  {n * bpp / us / 1e3:8.1f} GB/s", flush=True)
