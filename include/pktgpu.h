@@ -267,6 +267,13 @@ int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
  * Results are identical in every mode. */
 int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 
+/* Tuning knob: walk schedule.  0 = automatic (lockstep for indexed batches, waterfall for fixed
+ * stride), 1 = waterfall (each iteration advances the lanes in one state: one case per header
+ * when a wave's packets share a layout), 2 = lockstep (every lane advances one header per
+ * iteration: mixed chains in a wave cost their longest chain, not their number of distinct
+ * states).  Results are identical in every mode. */
+int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
+
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
  * Asynchronous on `stream`; returns after the launch. */

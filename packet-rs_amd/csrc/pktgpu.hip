@@ -37,6 +37,7 @@ struct pkt_ctx {
     int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
+    int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
     std::string err;
 };
 
@@ -291,7 +292,7 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
-template <int NCH, uint32_t GM>
+template <int NCH, uint32_t GM, int WK>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortLds& S, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own);
@@ -302,7 +303,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
 #ifndef PKTGPU_WAVES_PER_EU
 #define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
 #endif
-template <int NCH, uint32_t GM>
+template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
 void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
@@ -313,10 +314,10 @@ void parse_kernel(KParams p) {
     uint64_t off;
     uint32_t len;
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM>(p, lds, S, base, chunk, off, len, act);
+    parse_tile<NCH, GM, WK>(p, lds, S, base, chunk, off, len, act);
 }
 
-template <int NCH, uint32_t GM>
+template <int NCH, uint32_t GM, int WK>
 #ifndef PKTGPU_FAST_REG
 // 1: waves whose packets all take the fast path decode from registers, no LDS.  0 (default):
 // they stage and emit through LDS like mixed waves.  C2, same box: registers 28.7 us isolated /
@@ -393,7 +394,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
         // ---- unsorted: each lane walks and emits its own packet (no barrier: own LDS only)
         __builtin_amdgcn_wave_barrier();
         WalkResult r;
-        walk(pv_own, entry_state(p.entry), active_own && !fast, push, r);
+        walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r);
         if constexpr (NCH >= 4) {
             if (fast) fast_result(r);
         }
@@ -443,7 +444,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
             S.slot_off[slot][q] = (uint16_t)o;
         };
         WalkResult r;
-        walk(pvq, entry_state(p.entry), aq, push, r);
+        walk<WK>(pvq, entry_state(p.entry), aq, push, r);
         S.status[q] = (uint8_t)r.status;
         S.n[q] = (uint8_t)r.n;
         S.poff[q] = (uint16_t)r.payload_off;
@@ -502,7 +503,7 @@ __device__ __forceinline__ uint64_t wave_uniform64(uint64_t v) {
     return ((uint64_t)hi << 32) | lo;
 }
 
-template <int NCH, uint32_t GM>
+template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x;
@@ -560,7 +561,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
         if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
     };
     WalkResult r;
-    walk(pv, entry_state(p.entry), active, push, r);
+    walk<WK>(pv, entry_state(p.entry), active, push, r);
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
@@ -787,28 +788,37 @@ int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
 // How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
 enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
 
-template <int NCH, uint32_t GM>
+template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
     if (mode == M_SPAN) {
-        hipLaunchKernelGGL((parse_span_kernel<NCH, GM>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
+        hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), span_region(NCH), s, kp);
     } else {
         const size_t lds = window_lds(NCH) + (kp.sort ? sizeof(SortLds) : 0);
-        hipLaunchKernelGGL((parse_kernel<NCH, GM>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
+        hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }
     return hipGetLastError();
 }
 
+// Kernels are compiled per fully-requested column-group set; the lockstep walk (mixed traffic)
+// only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
-hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, hipStream_t s) {
+hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s) {
+    if (wk == 1) {
+        switch (gm) {
+            case G_CHAIN: return launch_mode<NCH, G_CHAIN, 1>(kp, mode, s);
+            case G_ALL: return launch_mode<NCH, G_ALL, 1>(kp, mode, s);
+            default: return launch_mode<NCH, G_RUNTIME, 1>(kp, mode, s);
+        }
+    }
     switch (gm) {
-        case G_CHAIN: return launch_mode<NCH, G_CHAIN>(kp, mode, s);
-        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP>(kp, mode, s);
+        case G_CHAIN: return launch_mode<NCH, G_CHAIN, 0>(kp, mode, s);
+        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP, 0>(kp, mode, s);
         case G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP:
-            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP>(kp, mode, s);
-        case G_ALL: return launch_mode<NCH, G_ALL>(kp, mode, s);
-        default: return launch_mode<NCH, G_RUNTIME>(kp, mode, s);
+            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP, 0>(kp, mode, s);
+        case G_ALL: return launch_mode<NCH, G_ALL, 0>(kp, mode, s);
+        default: return launch_mode<NCH, G_RUNTIME, 0>(kp, mode, s);
     }
 }
 
@@ -893,6 +903,7 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
     c->sort = 0;
     c->fast = 1;
     c->staging = 0;
+    c->walk = 0;
     *out = c;
     return PKT_SUCCESS;
 }
@@ -930,6 +941,12 @@ int pkt_ctx_set_fastpath(pkt_ctx_t* ctx, int enable) {
 int pkt_ctx_set_staging(pkt_ctx_t* ctx, int mode) {
     if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
     ctx->staging = mode;
+    return PKT_SUCCESS;
+}
+
+int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
+    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
+    ctx->walk = mode;
     return PKT_SUCCESS;
 }
 
@@ -981,6 +998,9 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Staging: wave spans when asked (not with the sorted path); per-lane windows otherwise
     // (auto: spans measured slower on C3 and C4).
     const int mode = (ctx->staging == 2 && ctx->sort != 1) ? M_SPAN : M_TILE;
+    // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
+    // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
+    const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
     const uint64_t kChunk = 1ull << 26;  // packets per launch (32-bit byte offsets in-kernel)
     for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kChunk) {
         const uint64_t cnt = std::min<uint64_t>(kChunk, b->n - i0);
@@ -1003,13 +1023,13 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kSize[c];
         kp.out = o;
-        if (nch <= 2) e = launch_gm<2>(kp, gm, mode, s);
-        else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, s);
-        else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, s);
-        else if (nch <= 8) e = launch_gm<8>(kp, gm, mode, s);
-        else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, s);
-        else if (nch <= 16) e = launch_gm<16>(kp, gm, mode, s);
-        else e = launch_gm<17>(kp, gm, mode, s);
+        if (nch <= 2) e = launch_gm<2>(kp, gm, mode, wk, s);
+        else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, wk, s);
+        else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, wk, s);
+        else if (nch <= 8) e = launch_gm<8>(kp, gm, mode, wk, s);
+        else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, wk, s);
+        else if (nch <= 16) e = launch_gm<16>(kp, gm, mode, wk, s);
+        else e = launch_gm<17>(kp, gm, mode, wk, s);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;

@@ -297,61 +297,155 @@ __device__ __forceinline__ void step(Lane& L, const PacketView& pv, Push& push) 
 // state of the first live lane (v_readlane), and every live lane in that state advances one
 // step under a SCALAR switch — a wave whose packets share a layout runs exactly one case per
 // header, a mixed wave one case per distinct state.
-// Walk schedule.  0: the waterfall above.  1: sweeps — the states in chain order (L2 -> L3 -> L4 ->
-// tunnel), each run while any lane is in it, repeated until no lane is live: a lane advances
-// through every forward edge of its chain within one sweep, and only the edges back to an earlier
-// state (tunnels to Ethernet/IP, IPv6 -> IPv4) wait for the next sweep.
-#ifndef PKTGPU_WALK_SWEEP
-#define PKTGPU_WALK_SWEEP 0
-#endif
+// ---- lockstep step: one header for a lane in ANY state, with the per-state constants read from
+// packed tables and the next state chosen by selects (no divergent branch per state).
+// Semantics are exactly step<S>'s: same checks in the same order, same records.
 
-template <uint32_t S, class Push>
-__device__ __forceinline__ void sweep_state(Lane& L, const PacketView& pv, Push& push) {
-    while (__ballot(L.live && L.st == S)) {
-        if (L.live && L.st == S) {
-            if (++L.steps > PKT_MAX_HDRS + 3) fail(L, PKT_DEPTH_LIMIT);
-            else step<S>(L, pv, push);
-        }
-    }
+// 6-bit fields per state (states 0..9 in lo, 10..18 in hi): header size (PARSE: the 14 bytes
+// fast.rs:6 reads; ACCEPT: 0).
+constexpr uint64_t pack6(const uint32_t (&v)[10], int k0) {
+    uint64_t r = 0;
+    for (int i = 0; i < 10; i++)
+        if (k0 + i < 19) r |= (uint64_t)(v[i] & 63u) << (6 * i);
+    return r;
+}
+//                                    PARSE DOT3 LLC SNAP ETHER VLAN MPLS BOS IPV4 IPV6
+constexpr uint32_t kSzLo[10]       = {14,   14,  3,  5,   14,   4,   4,   4,  20,  40};
+//                                    GRE  ER2 ER3 ARP ICMP TCP UDP VXLAN ACCEPT
+constexpr uint32_t kSzHi[10]       = {4,   8,  12, 28, 4,   20, 8,  8,    0, 0};
+constexpr uint32_t kTyLo[10]       = {0, PKT_HDR_DOT3, PKT_HDR_LLC, PKT_HDR_SNAP, PKT_HDR_ETHER, PKT_HDR_VLAN,
+                                      PKT_HDR_MPLS, PKT_HDR_MPLS, PKT_HDR_IPV4, PKT_HDR_IPV6};
+constexpr uint32_t kTyHi[10]       = {PKT_HDR_GRE, PKT_HDR_ERSPAN2, PKT_HDR_ERSPAN3, PKT_HDR_ARP, PKT_HDR_ICMP,
+                                      PKT_HDR_TCP, PKT_HDR_UDP, PKT_HDR_VXLAN, 0, 0};
+// byte offset of the big-endian dword holding the dispatch field
+//                                    PARSE DOT3 LLC SNAP ETHER VLAN MPLS BOS IPV4 IPV6
+constexpr uint32_t kDwLo[10]       = {12,   0,   0,  0,   12,   2,   0,   4,  8,   4};
+//                                    GRE  ER2 ER3 ARP ICMP TCP UDP VXLAN ACCEPT
+constexpr uint32_t kDwHi[10]       = {0,   0,  8,  0,  0,   0,  2,  0,    0, 0};
+constexpr uint64_t kSz0 = pack6(kSzLo, 0), kSz1 = pack6(kSzHi, 10);
+constexpr uint64_t kTy0 = pack6(kTyLo, 0), kTy1 = pack6(kTyHi, 10);
+constexpr uint64_t kDw0 = pack6(kDwLo, 0), kDw1 = pack6(kDwHi, 10);
+
+__device__ __forceinline__ uint32_t tab6(uint64_t lo, uint64_t hi, uint32_t st) {
+    const bool h = st >= 10u;
+    const uint64_t t = h ? hi : lo;
+    return (uint32_t)(t >> (6u * (h ? st - 10u : st))) & 63u;
+}
+
+// rec() with a run-time type
+template <class Push>
+__device__ __forceinline__ void rec_rt(Lane& L, uint32_t t, uint32_t off, Push& push) {
+    push(L.r.n, t, off);
+    L.r.n++;
+    L.r.mask |= 1u << t;
+    const int32_t o = (int32_t)off;
+    if (t == PKT_HDR_ETHER && L.r.f_eth < 0) L.r.f_eth = o;
+    if (t == PKT_HDR_VLAN && L.r.f_vlan < 0) L.r.f_vlan = o;
+    if (t == PKT_HDR_IPV4 && L.r.f_ipv4 < 0) L.r.f_ipv4 = o;
+    if (t == PKT_HDR_IPV6 && L.r.f_ipv6 < 0) L.r.f_ipv6 = o;
+    if (t == PKT_HDR_TCP && L.r.f_tcp < 0) L.r.f_tcp = o;
+    if (t == PKT_HDR_UDP && L.r.f_udp < 0) L.r.f_udp = o;
 }
 
 template <class Push>
+__device__ __forceinline__ void gstep(Lane& L, const PacketView& pv, Push& push) {
+    const uint32_t st = L.st, o = L.o, len = pv.len;
+    if (st == S_ACCEPT) {  // fast.rs:223-227
+        L.r.payload_off = o;
+        L.live = false;
+        return;
+    }
+    const uint32_t sz = tab6(kSz0, kSz1, st);
+    if (o + sz > len) { fail(L, PKT_TRUNCATED); return; }  // `&arr[0..X::size()]` (PARSE: arr[12..13])
+    if (st != S_PARSE && L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+    // the dispatch dword (bytes past the header are read but never used)
+    const uint32_t D = bswap32(pv.le(o + tab6(kDw0, kDw1, st), 4));
+    const uint32_t hw = D >> 16;
+    // next state of every kind, then the one for this state
+    const uint32_t et_next = etype_next(hw);
+    const bool v6 = st == S_IPV6;
+    const uint32_t ip_next = ipproto_next(v6 ? (D >> 8) & 0xFFu : hw & 0xFFu, v6);
+    uint32_t nx = S_ACCEPT;  // SNAP, ARP, ICMP, TCP
+    nx = (st == S_PARSE) ? (hw < 1500u ? S_DOT3 : S_ETHER) : nx;
+    nx = (st == S_DOT3) ? S_LLC : nx;
+    nx = (st == S_LLC) ? ((D >> 8) == 0xAAAA03u ? S_SNAP : S_ACCEPT) : nx;
+    nx = (st == S_ETHER || st == S_VLAN) ? et_next : nx;
+    nx = (st == S_MPLS) ? (((D >> 8) & 1u) ? S_MPLS_BOS : S_MPLS) : nx;
+    nx = (st == S_MPLS_BOS) ? ((D >> 28) == 4u ? S_IPV4 : ((D >> 28) == 6u ? S_IPV6 : S_ETHER)) : nx;
+    nx = (st == S_IPV4 || st == S_IPV6) ? ip_next : nx;
+    nx = (st == S_GRE) ? gre_next(D & 0xFFFFu) : nx;
+    nx = (st == S_ERSPAN2 || st == S_ERSPAN3 || st == S_VXLAN) ? S_ETHER : nx;
+    nx = (st == S_UDP) ? (hw == 4789u ? S_VXLAN : S_ACCEPT) : nx;
+    if (st == S_PARSE) {
+        L.st = nx;
+        return;
+    }
+    // fast.rs:74-83: arr[MPLS::size()] must exist (Q3)
+    if (st == S_MPLS_BOS && o + 5 > len) { fail(L, PKT_TRUNCATED); return; }
+    rec_rt(L, tab6(kTy0, kTy1, st), o, push);
+    uint32_t q = o + sz;
+    if (st == S_GRE) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
+        const uint32_t c = D >> 31, k = (D >> 29) & 1u, sb = (D >> 28) & 1u;
+        if (c) {
+            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+            if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+        }
+        const uint32_t oc = q;
+        q += 4u * c;
+        if (k) {
+            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+            if (L.r.n + c >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+        }
+        const uint32_t okey = q;
+        q += 4u * k;
+        if (sb) {
+            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
+            if (L.r.n + c + k >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+        }
+        const uint32_t oseq = q;
+        q += 4u * sb;
+        if (sb) rec_rt(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push);
+        if (k) rec_rt(L, PKT_HDR_GRE_KEY, okey, push);
+        if (c) rec_rt(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push);
+    } else if (st == S_ERSPAN3 && (D & 1u)) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
+        if (q + 8 > len) { fail(L, PKT_TRUNCATED); return; }
+        if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
+        rec_rt(L, PKT_HDR_ERSPAN_PLATFORM, q, push);
+        q += 8;
+    }
+    L.o = q;
+    L.st = nx;
+}
+
+// The walk.  WK = 0, waterfall: each iteration takes the state of the first live lane and every
+// live lane in that state advances one step under a SCALAR switch — a wave whose packets share a
+// layout runs exactly one case per header, a mixed wave one case per distinct (state, depth).
+// WK = 1, lockstep: every live lane advances one header per iteration through gstep() — a mixed
+// wave runs (its longest chain + 2) iterations (C4: 10 instead of ~38).
+template <int WK, class Push>
 __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool active, Push&& push,
                                      WalkResult& out) {
-#if PKTGPU_WALK_SWEEP
-    Lane L;
-    L.st = state;
-    L.o = 0;
-    L.steps = 0;
-    L.live = active;
-    L.r.status = PKT_OK;
-    L.r.n = 0;
-    L.r.payload_off = 0;
-    L.r.mask = 0;
-    L.r.f_eth = L.r.f_vlan = L.r.f_ipv4 = L.r.f_ipv6 = L.r.f_tcp = L.r.f_udp = -1;
-    while (__ballot(L.live)) {
-        sweep_state<S_PARSE>(L, pv, push);
-        sweep_state<S_DOT3>(L, pv, push);
-        sweep_state<S_LLC>(L, pv, push);
-        sweep_state<S_SNAP>(L, pv, push);
-        sweep_state<S_ETHER>(L, pv, push);
-        sweep_state<S_VLAN>(L, pv, push);
-        sweep_state<S_MPLS>(L, pv, push);
-        sweep_state<S_MPLS_BOS>(L, pv, push);
-        sweep_state<S_ARP>(L, pv, push);
-        sweep_state<S_IPV6>(L, pv, push);
-        sweep_state<S_IPV4>(L, pv, push);
-        sweep_state<S_ICMP>(L, pv, push);
-        sweep_state<S_TCP>(L, pv, push);
-        sweep_state<S_UDP>(L, pv, push);
-        sweep_state<S_VXLAN>(L, pv, push);
-        sweep_state<S_GRE>(L, pv, push);
-        sweep_state<S_ERSPAN2>(L, pv, push);
-        sweep_state<S_ERSPAN3>(L, pv, push);
-        sweep_state<S_ACCEPT>(L, pv, push);
+    if constexpr (WK == 1) {
+        Lane L;
+        L.st = state;
+        L.o = 0;
+        L.steps = 0;
+        L.live = active;
+        L.r.status = PKT_OK;
+        L.r.n = 0;
+        L.r.payload_off = 0;
+        L.r.mask = 0;
+        L.r.f_eth = L.r.f_vlan = L.r.f_ipv4 = L.r.f_ipv6 = L.r.f_tcp = L.r.f_udp = -1;
+        while (__ballot(L.live)) {
+            if (L.live) {
+                // at most PKT_MAX_HDRS headers + parse + accept + the failing step
+                if (++L.steps > PKT_MAX_HDRS + 3) fail(L, PKT_DEPTH_LIMIT);
+                else gstep(L, pv, push);
+            }
+        }
+        out = L.r;
+        return;
     }
-    out = L.r;
-#else
     Lane L;
     L.st = state;
     L.o = 0;
@@ -401,7 +495,6 @@ __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool 
         }
     }
     out = L.r;
-#endif
 }
 
 }  // namespace pktgpu

@@ -58,6 +58,7 @@ SIGNATURES = {
     "pkt_ctx_set_sort": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_fastpath": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_staging": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pkt_ctx_set_walk": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
     "pkt_parse_host": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.POINTER(PktOut),

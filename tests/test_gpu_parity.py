@@ -493,3 +493,27 @@ def test_staging_modes_bit_exact(P, staging):
     finally:
         P.set_staging(0)
         P.set_window(0)
+
+
+@pytest.mark.parametrize("walk", [1, 2])
+def test_walk_modes_bit_exact(P, walk):
+    """Waterfall (1) and lockstep (2) walks give identical columns on every mix, every entry,
+    truncations, depth limits and GRE option combinations; and with wave spans."""
+    P.set_walk(walk)
+    try:
+        _mode_cases(P, f"wk{walk}")
+        rng = np.random.default_rng(61)
+        tm = [p.to_vec() for p in gen.reference_22_packets()]
+        for entry in schema.ENTRIES:
+            pk = [t[int(rng.integers(0, 14)):] for t in tm] + [rng.integers(0, 256, int(rng.integers(0, 80)), dtype=np.uint8).tobytes() for _ in range(300)]
+            b = b"".join(pk)
+            ln = np.array([len(x) for x in pk], np.uint32)
+            of = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+            both(P, np.frombuffer(b + bytes(16), np.uint8), len(pk), offsets=of, lens=ln, entry=entry,
+                 label=f"{entry} wk{walk}")
+        P.set_staging(2)
+        buf, offs, lens = gen.gen_c4(20011, seed=62)
+        both(P, buf, len(offs), offsets=offs, lens=lens, label=f"c4 span wk{walk}")
+    finally:
+        P.set_walk(0)
+        P.set_staging(0)
