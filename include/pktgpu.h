@@ -130,7 +130,8 @@ typedef struct pkt_batch {
  *
  * Chain columns = PacketSlice (lib.rs:136-140, packet.rs:714-761):
  *   hdr_type/hdr_off are slot-major: slot j of packet i lives at [j*n + i]; slots
- *   j < n_hdrs[i] hold the chain; later slots are not written.  List order is the reference's `Vec::insert(0, ..)` order,
+ *   j < n_hdrs[i] hold the chain; later slots are unspecified (not written for a parsed packet;
+ *   a packet that fails may have written some before its failing header).  List order is the reference's `Vec::insert(0, ..)` order,
  *   i.e. wire order except GRE options (Q2: GRE, SeqNum, Key, ChksumOffset).
  *   hdr_off is the header's byte offset from the start of the packet (the Slice's
  *   pointer, headers.rs:187-192); payload_off/payload_len = PacketSlice::payload().
