@@ -255,8 +255,8 @@ int         pkt_ctx_set_window(pkt_ctx_t *ctx, uint32_t window_bytes);
  * more than the uniform waves save on the measured mixes), 1 = always, 2 = never. */
 int         pkt_ctx_set_sort(pkt_ctx_t *ctx, int mode);
 /* Fast path (default on).  For entries PARSE and ETHERNET, a packet that starts on a 16-byte
- * boundary and whose first bytes read Ether(0x0800) / IPv4 / UDP (dst != 4789) or TCP, long
- * enough for every header, has its chain decided by three compares on the registers its bytes
+ * boundary and whose first bytes read Ether / 0-2 x Vlan / IPv4 / UDP (dst != 4789) or TCP, long
+ * enough for every header, has its chain decided by a few compares on the registers its bytes
  * were loaded into, so it skips the walk.  Results are identical to the walk's (the same fast.rs
  * path; the parity tests run with it forced on and off).  0 = off, 1 = on. */
 int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);

@@ -329,48 +329,63 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
                                            bool active_own) {
     const uint32_t t = threadIdx.x;
     const uint32_t i_own = base + t;
-    // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose bytes 12-13 = 0x0800,
-    // byte 23 = 17 with bytes 36-37 != 4789 and len >= 42, or byte 23 = 6 and len >= 54, takes
-    // exactly fast.rs's Ether -> IPv4 -> UDP|TCP -> accept path (no bound or depth check can
-    // fail), so it needs neither the LDS window nor the walk.
-    bool fast = false;
+    // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose EtherType chain is
+    // 0x0800, 0x8100 0x0800 or 0x8100 0x8100 0x0800 (bytes 12, 16, 20: v = 0..2 VLAN tags), whose
+    // IPv4 protocol (byte 23 + 4v) is 17 with a UDP dst port (bytes 36 + 4v) != 4789 and
+    // len >= 42 + 4v, or 6 with len >= 54 + 4v, takes exactly fast.rs's Ether -> Vlan{v} -> IPv4 ->
+    // UDP|TCP -> accept path (no bound or depth check can fail on it), so a few compares on the
+    // loaded registers decide its whole chain: it skips the walk.
+    bool fast = false, fudp = false;
+    uint32_t fv = 0;
     if constexpr (NCH >= 4) {
         // (not with the sorted path: a lane there walks another lane's staged packet)
-        if (p.fast && !p.sort && active_own && (off_own & 15) == 0 && (chunk[0].w & 0xFFFFu) == 0x0008u) {
-            const uint32_t proto = chunk[1].y >> 24;
-            fast = (proto == 17u && len_own >= 42u && (chunk[2].y & 0xFFFFu) != 0xB512u) ||
-                   (proto == 6u && len_own >= 54u);
+        if (p.fast && !p.sort && active_own && (off_own & 15) == 0) {
+            const uint32_t e0 = chunk[0].w & 0xFFFFu, e1 = chunk[1].x & 0xFFFFu, e2 = chunk[1].y & 0xFFFFu;
+            const bool v0 = e0 == 0x0008u;                    // little-endian 0x0800
+            const bool v1 = e0 == 0x0081u && e1 == 0x0008u;   // 0x8100, 0x0800
+            const bool v2 = e0 == 0x0081u && e1 == 0x0081u && e2 == 0x0008u;
+            fv = v1 ? 1u : (v2 ? 2u : 0u);
+            const uint32_t proto = (v0 ? chunk[1].y : v1 ? chunk[1].z : chunk[1].w) >> 24;
+            const uint32_t dport = (v0 ? chunk[2].y : v1 ? chunk[2].z : chunk[2].w) & 0xFFFFu;
+            const uint32_t l4 = 34u + 4u * fv;
+            fudp = proto == 17u;
+            fast = (v0 || v1 || v2) && ((fudp && len_own >= l4 + 8u && dport != 0xB512u) ||
+                                        (proto == 6u && len_own >= l4 + 20u));
         }
     }
     // Fast lanes skip the walk; all lanes stage their window and emit from LDS together (one
-    // store per column per wave).  With PKTGPU_FAST_REG a wave whose every packet is fast
-    // decodes from registers instead (wave-uniform branch).
+    // store per column per wave).  With PKTGPU_FAST_REG a wave whose every packet is fast and
+    // untagged decodes from registers instead (wave-uniform branch).
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
     auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
         if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i_own] = (uint8_t)ty;
         if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i_own] = (uint16_t)o;
     };
-    // fast.rs:5-12 (0x0800 >= 1500) -> parse_ethernet 35-48 (0x0800) -> parse_ipv4 84-98
-    // (17 / 6) -> parse_udp 208-217 (dst != 4789) | parse_tcp 203-207 -> accept 223-227
-    auto fast_result = [&](WalkResult& r) {
-        const bool udp = (chunk[1].y >> 24) == 17u;
+    // fast.rs:5-12 (>= 1500) -> parse_ethernet 35-48 (0x8100 -> parse_vlan 49-62, repeated;
+    // 0x0800) -> parse_ipv4 84-98 (17 / 6) -> parse_udp 208-217 (dst != 4789) | parse_tcp 203-207
+    // -> accept 223-227
+    auto fast_result = [&](WalkResult& r, uint32_t v) {
+        const uint32_t l4 = 34u + 4u * v;
         r.status = PKT_OK;
-        r.n = 3;
-        r.payload_off = udp ? 42u : 54u;
-        r.mask = (1u << PKT_HDR_ETHER) | (1u << PKT_HDR_IPV4) | (udp ? 1u << PKT_HDR_UDP : 1u << PKT_HDR_TCP);
+        r.n = 3 + v;
+        r.payload_off = l4 + (fudp ? 8u : 20u);
+        r.mask = (1u << PKT_HDR_ETHER) | (1u << PKT_HDR_IPV4) | (fudp ? 1u << PKT_HDR_UDP : 1u << PKT_HDR_TCP) |
+                 (v ? 1u << PKT_HDR_VLAN : 0u);
         r.f_eth = 0;
-        r.f_vlan = -1;
-        r.f_ipv4 = 14;
+        r.f_vlan = v ? 14 : -1;
+        r.f_ipv4 = (int32_t)(14u + 4u * v);
         r.f_ipv6 = -1;
-        r.f_tcp = udp ? -1 : 34;
-        r.f_udp = udp ? 34 : -1;
+        r.f_tcp = fudp ? -1 : (int32_t)l4;
+        r.f_udp = fudp ? (int32_t)l4 : -1;
         push(0, PKT_HDR_ETHER, 0);
-        push(1, PKT_HDR_IPV4, 14);
-        push(2, udp ? PKT_HDR_UDP : PKT_HDR_TCP, 34);
+        if (v >= 1) push(1, PKT_HDR_VLAN, 14);
+        if (v >= 2) push(2, PKT_HDR_VLAN, 18);
+        push(1 + v, PKT_HDR_IPV4, 14u + 4u * v);
+        push(2 + v, fudp ? PKT_HDR_UDP : PKT_HDR_TCP, l4);
     };
     if constexpr (NCH >= 4) {
-        if (PKTGPU_FAST_REG && !p.sort && __ballot(fast) == __ballot(active_own)) {
+        if (PKTGPU_FAST_REG && !p.sort && __ballot(fast && fv == 0) == __ballot(active_own)) {
             if (!active_own) return;
             RegView<NCH> rv;
 #pragma unroll
@@ -381,7 +396,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
                 rv.w[4 * c + 3] = chunk[c].w;
             }
             WalkResult r;
-            fast_result(r);
+            fast_result(r, 0u);
             emit_chain<GM>(out, i_own, len_own, r);
             emit_fields<GM>(out, i_own, rv, r, true);
             return;
@@ -396,7 +411,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
         WalkResult r;
         walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r);
         if constexpr (NCH >= 4) {
-            if (fast) fast_result(r);
+            if (fast) fast_result(r, fv);
         }
         if (!active_own) return;
         emit_chain<GM>(out, i_own, len_own, r);

@@ -517,3 +517,48 @@ def test_walk_modes_bit_exact(P, walk):
     finally:
         P.set_walk(0)
         P.set_staging(0)
+
+
+def _vlan_fastpath_mix(n, seed):
+    """C3-shaped packets (0-2 VLAN tags, IPv4, TCP|UDP) with per-packet lengths around every
+    fast-path bound (42/54 + 4v), UDP dst 4789 at the tag-shifted offset, a third tag, and
+    EtherTypes after the tags mutated, so every branch of the VLAN fast-path classifier is hit."""
+    rng = np.random.default_rng(seed)
+    a = gen.gen_c3(n, seed=seed)
+    tags = np.zeros(n, np.int64)
+    tags[(a[:, 12] == 0x81) & (a[:, 13] == 0)] = 1
+    tags[(tags == 1) & (a[:, 16] == 0x81) & (a[:, 17] == 0)] = 2
+    l4 = 34 + 4 * tags
+    udp = a[np.arange(n), 23 + 4 * tags] == 17
+    r = rng.random(n)
+    m = (r < 0.05) & udp  # VXLAN port at the shifted UDP dst
+    a[np.nonzero(m)[0], (l4 + 2)[m]] = 0x12
+    a[np.nonzero(m)[0], (l4 + 3)[m]] = 0xB5
+    m = (r >= 0.05) & (r < 0.08) & (tags == 2)  # a third tag
+    a[np.nonzero(m)[0], 20] = 0x81
+    a[np.nonzero(m)[0], 21] = 0x00
+    m = (r >= 0.08) & (r < 0.11) & (tags >= 1)  # EtherType after the first tag neither IPv4 nor Vlan
+    a[np.nonzero(m)[0], 16] = 0x86
+    a[np.nonzero(m)[0], 17] = 0xDD
+    m = (r >= 0.11) & (r < 0.14)  # protocol neither TCP nor UDP
+    a[np.nonzero(m)[0], (23 + 4 * tags)[m]] = 47
+    bound = l4 + np.where(udp, 8, 20)
+    lens = np.where(rng.random(n) < 0.6, bound + rng.integers(-3, 3, n), rng.integers(0, 129, n))
+    return a, np.clip(lens, 0, 128).astype(np.uint32)
+
+
+@pytest.mark.parametrize("fast", [1, 0])
+def test_vlan_fastpath_boundaries(P, fast):
+    """The fast path for Ether/0-2 Vlan/IPv4/TCP|UDP agrees with the walk (and the oracle) at every
+    length bound, shifted VXLAN port, third tag and non-IPv4 EtherType after a tag."""
+    P.set_fastpath(fast)
+    try:
+        n = 60001
+        a, lens = _vlan_fastpath_mix(n, seed=70 + fast)
+        for entry in ("parse", "parse_ethernet"):
+            both(P, a, n, stride=128, lens=lens, entry=entry, label=f"vlan {entry} f{fast}")
+        both(P, a, n, stride=128, label=f"vlan full f{fast}")
+        both(P, a, n, stride=128, lens=lens, columns=["chain", "vlan", "ipv4", "tcp", "udp"],
+             label=f"vlan cols f{fast}")
+    finally:
+        P.set_fastpath(1)
