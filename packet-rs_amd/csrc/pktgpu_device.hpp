@@ -24,7 +24,10 @@
 namespace pktgpu {
 
 constexpr int kWave = 64;
-constexpr int kWavesPerBlock = 4;
+#ifndef PKTGPU_WAVES_PER_BLOCK
+#define PKTGPU_WAVES_PER_BLOCK 4
+#endif
+constexpr int kWavesPerBlock = PKTGPU_WAVES_PER_BLOCK;
 constexpr int kBlock = kWave * kWavesPerBlock;
 
 // Walk states = the parse_* functions of fast.rs (+ accept / done markers).
