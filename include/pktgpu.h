@@ -277,7 +277,10 @@ int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
 
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
- * Asynchronous on `stream`; returns after the launch. */
+ * Asynchronous on `stream`; returns after the launch.  `batch` and `out` may also point into pinned
+ * host memory from pkt_host_alloc (mapped into the device): the kernel then reads and writes it
+ * over the link directly — zero copy, still asynchronous (see pkt_parse_host for the blocking
+ * form; pkt_ctx_set_staging(ctx, 2) suits host-resident indexed batches). */
 int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
                     const pkt_out_t *out, void *stream);
 

@@ -972,17 +972,18 @@ int pkt_ctx_set_sort(pkt_ctx_t* ctx, int mode) {
 }
 
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias);
+                      void* stream, uint64_t off_bias, int staging);
 
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
     // the kernel reads whole 16-byte chunks, clamped to the last one of the slab
     if (b && b->n && b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
-    return parse_impl(ctx, b, entry, out, stream, 0);
+    return parse_impl(ctx, b, entry, out, stream, 0, ctx ? ctx->staging : 0);
 }
 
+// `staging` = the ctx's knob, or the host path's override (wave spans over the link).
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias) {
+                      void* stream, uint64_t off_bias, int staging) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -1012,7 +1013,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // Staging: wave spans when asked (not with the sorted path); per-lane windows otherwise
     // (auto: spans measured slower on C3 and C4).
-    const int mode = (ctx->staging == 2 && ctx->sort != 1) ? M_SPAN : M_TILE;
+    const int mode = (staging == 2 && ctx->sort != 1) ? M_SPAN : M_TILE;
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
@@ -1095,10 +1096,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
             // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
             // for a deep header (per-lane windows would, one dependent PCIe read each)
-            const int st = ctx->staging;
-            if (st == 0) ctx->staging = 2;
-            int rc = parse_impl(ctx, &db, entry, &dout, hp.s[0], 0);
-            ctx->staging = st;
+            int rc = parse_impl(ctx, &db, entry, &dout, hp.s[0], 0, ctx->staging == 0 ? 2 : ctx->staging);
             if (rc != PKT_SUCCESS) return rc;
             e = hipStreamSynchronize(hp.s[0]);
             return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipStreamSynchronize");
@@ -1181,7 +1179,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         uint8_t** dcol = reinterpret_cast<uint8_t**>(&dout);
         for (int c = 0; c < 49; c++) dcol[c] = hcol[c] ? hp.out[q] + col_off[c] : nullptr;
         // (the device buffer always has >= 16 readable bytes, so a view shorter than 16 is safe)
-        rc = parse_impl(ctx, &db, entry, &dout, s, b->offsets ? base : 0);
+        rc = parse_impl(ctx, &db, entry, &dout, s, b->offsets ? base : 0, ctx->staging);
         if (rc != PKT_SUCCESS) break;
         // out: every requested column into its host rows [lo, hi)
         for (int c = 0; c < 49 && e == hipSuccess; c++) {
