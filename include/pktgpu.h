@@ -357,6 +357,14 @@ int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride
 int pkt_pcap_index(const uint8_t *buf, uint64_t len, uint64_t *offsets, uint32_t *lens,
                    uint64_t cap, uint64_t *n_out);
 
+/* pkt_pcap_index for a pcap file resident in DEVICE memory (`buf` 16-byte aligned, readable up to
+ * round_up(len, 16)): same records, count, cap behaviour and errors, with `offsets` / `lens` in
+ * device memory — ready for an indexed pkt_batch_t over the same buffer.  The sequential record
+ * chain is recovered per 4 KiB region by a speculative guess plus exact fix-up rounds
+ * (pktgpu_pcap.hip).  Blocking: returns once *n_out is known (work is ordered on `stream`). */
+int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint64_t *offsets,
+                          uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
+
 /* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
 uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
 

@@ -6,6 +6,7 @@
 //                         extraction of the first Ether/Vlan/IPv4/IPv6/TCP/UDP (Q11).
 //   extract_kernel        batched make_header! getter for arbitrary (type, occurrence, bits).
 //   ipv4_csum_kernel      Packet::ipv4_checksum over a strided array of 20-byte headers.
+// (the device pcap indexer is in pktgpu_pcap.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -14,32 +15,10 @@
 #include <string>
 #include <type_traits>
 
+#include "pktgpu_ctx.hpp"
 #include "pktgpu_device.hpp"
 
 using namespace pktgpu;
-
-// Device buffers and streams of the host-memory pipeline (pkt_parse_host), grown on demand.
-struct HostPipe {
-    static constexpr int kSlots = 3;
-    bool init = false;
-    hipStream_t s[kSlots] = {};
-    uint8_t* slab[kSlots] = {};
-    uint64_t* offs[kSlots] = {};
-    uint32_t* lens[kSlots] = {};
-    uint8_t* out[kSlots] = {};
-    uint64_t slab_cap = 0, pkt_cap = 0, out_cap = 0;  // bytes per slot (pkt_cap: offs and lens)
-};
-
-struct pkt_ctx {
-    int device;
-    HostPipe hp;
-    uint32_t window;  // 0 = auto
-    int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
-    int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
-    int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
-    int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
-    std::string err;
-};
 
 namespace {
 
@@ -790,16 +769,6 @@ __global__ __launch_bounds__(256) void ipv4_csum_kernel(const uint8_t* hdrs, uin
     out[i] = (uint16_t)~s;
 }
 
-int fail(pkt_ctx* ctx, int code, const char* msg) {
-    if (ctx) ctx->err = msg;
-    return code;
-}
-
-int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
-    if (ctx) ctx->err = std::string(what) + ": " + hipGetErrorString(e);
-    return PKT_ERR_HIP;
-}
-
 // How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
 enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
 
@@ -924,6 +893,12 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
 }
 
 int pkt_ctx_destroy(pkt_ctx_t* ctx) {
+    if (ctx && (ctx->pc.buf || ctx->pc.ctl)) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->pc.buf);
+        (void)hipHostFree(ctx->pc.ctl);
+    }
     if (ctx && ctx->hp.init) {
         (void)hipSetDevice(ctx->device);
         for (int k = 0; k < HostPipe::kSlots; k++) {

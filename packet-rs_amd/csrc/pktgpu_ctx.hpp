@@ -1,0 +1,50 @@
+// pktgpu_ctx.hpp — the pkt_ctx behind the C ABI's opaque handle, shared by the kernel sources
+// (pktgpu.hip: parse / extract / rewrite; pktgpu_pcap.hip: the device pcap indexer).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "../../include/pktgpu.h"
+
+// Device buffers and streams of the host-memory pipeline (pkt_parse_host), grown on demand.
+struct HostPipe {
+    static constexpr int kSlots = 3;
+    bool init = false;
+    hipStream_t s[kSlots] = {};
+    uint8_t* slab[kSlots] = {};
+    uint64_t* offs[kSlots] = {};
+    uint32_t* lens[kSlots] = {};
+    uint8_t* out[kSlots] = {};
+    uint64_t slab_cap = 0, pkt_cap = 0, out_cap = 0;  // bytes per slot (pkt_cap: offs and lens)
+};
+
+// Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.
+struct PcapScratch {
+    void* buf = nullptr;   // regions x (entry u64, exit u64, count u32, err u32) + record lists + scan
+    uint64_t bytes = 0;
+    uint64_t* ctl = nullptr;  // pinned host words the indexer reads back (change count, totals)
+};
+
+struct pkt_ctx {
+    int device;
+    HostPipe hp;
+    PcapScratch pc;
+    uint32_t window;  // 0 = auto
+    int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
+    int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
+    int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
+    int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
+    std::string err;
+};
+
+inline int fail(pkt_ctx* ctx, int code, const char* msg) {
+    if (ctx) ctx->err = msg;
+    return code;
+}
+
+inline int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
+    if (ctx) ctx->err = std::string(what) + ": " + hipGetErrorString(e);
+    return PKT_ERR_HIP;
+}

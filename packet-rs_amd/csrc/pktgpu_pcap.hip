@@ -1,0 +1,475 @@
+// pktgpu_pcap.hip — the device pcap indexer: pkt_pcap_index_device finds
+// the record boundaries of a pcap file that is already in HBM and writes the (data offset,
+// incl_len) pairs an indexed batch takes (pkt_batch_t.offsets / lens), so a capture copied to the
+// device as-is goes to pkt_parse_batch without a host pass over it.
+//
+// Format: tests/pcap.rs:7-37 (24-byte global header with LE magic d4 c3 b2 a1, then records of a
+// 16-byte header {ts_sec, ts_usec, incl_len, orig_len} + incl_len bytes).  Result and error
+// behaviour are pkt_pcap_index's (pktgpu_host.cpp): records are taken while 16 header bytes
+// remain; a record running past the end is an error; a shorter tail is ignored.
+//
+// The record chain is sequential (each header says where the next one starts), so the file is cut
+// into 4 KiB regions, one wave each, and the chain is recovered by speculation plus a fix-up:
+//   GUESS   a block stages 4 consecutive regions (16 KiB + 16 B) in LDS; each wave finds the
+//           first offset of its region from which a chain of plausible record headers runs (64
+//           offsets per step, one per lane; hops past the staged block read global memory), walks
+//           the records from there and keeps (entry, exit, count, error) and the records' offsets
+//           in the region (u16 list).  Region 0's entry is 24, by definition.
+//   REPAIR  one thread per region compares its entry with the exit of the nearest non-empty
+//           region to its left.  A region that disagrees while that neighbour agrees with its own
+//           left is queued; the block's waves re-walk each queued region from that exit and chase
+//           on into the following regions until an exit meets the next region's stored entry.
+//           Every region left of the first disagreement is exact (region 0 is, and each agrees
+//           with an exact left), so the first queued chase is exact and no round ends without
+//           fixing at least that region; a round in which no region disagrees is the exact fixed
+//           point — the true chain, whatever the guesses were.
+//   SCAN    exclusive prefix of the per-region counts (per 1024 regions; the last block to finish
+//           scans the block totals).
+//   EMIT    256 threads write 16 regions' records at their prefix: offset = pos + 16, incl_len =
+//           next pos - pos - 16 (the last one from the region's exit); the file is not re-read.
+// HBM traffic ≈ the file once + 2 B/record (the list) written and read + 12 B/record of output.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "pktgpu_ctx.hpp"
+
+namespace {
+
+constexpr uint32_t kRegion = 4096;               // bytes of record starts per region
+constexpr uint32_t kMaxRec = kRegion / 16;       // records per region (each >= 16 B apart)
+constexpr int kWaves = 4;                         // waves per 256-thread block
+constexpr uint32_t kBlockBytes = kWaves * kRegion;
+constexpr uint32_t kScanBlock = 1024;             // regions per first-level scan block
+constexpr uint32_t kEmitRegions = 16;             // regions per emit block
+constexpr int kLookback = 64;                     // empty regions skipped when finding an entry
+constexpr int kChaseMax = 256;                    // regions one repair chase may rewrite
+constexpr int kMinHops = 3, kMaxHops = 8;         // guess chain length
+constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec within a day
+constexpr uint32_t kPassSlots = 64;               // passes with their own control words
+
+// Control words (device, zeroed once per call): [0] magic is d4 c3 b2 a1; then per pass p (slot
+// p % 64): [8 + 8s + 2r] regions that disagreed in round r, [9 + 8s + 2r] K - first such region
+// (max; 0 = none), [12 + 8s] a region's walk hit a record running past the end, [13 + 8s] the
+// record total, [14 + 8s] the scan's block ticket.
+constexpr uint32_t kCtlWords = 8 + 8 * kPassSlots;
+
+struct Scratch {
+    uint64_t* entry;   // first record start >= region start (may lie past the region)
+    uint64_t* exit;    // first record start >= region end, as walked from entry
+    uint32_t* cnt;     // records starting in the region
+    uint32_t* err;     // the walk met a record running past the end of the file
+    uint32_t* pre;     // exclusive prefix of cnt within its scan block
+    uint64_t* bpre;    // exclusive prefix of the scan blocks
+    uint16_t* list;    // [region][kMaxRec] record offsets relative to the region base
+    uint64_t* ctl;     // control words above
+};
+
+__device__ __forceinline__ uint32_t lane_id() {
+    return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+}
+
+// Order a wave's LDS writes before its other lanes' reads (no block barrier).
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t ld32(const uint32_t* lw, uint32_t o) {
+    // Little-endian u32 at any byte offset of the staged bytes (two dwords + v_alignbyte).
+    return __builtin_amdgcn_alignbyte(lw[(o >> 2) + 1], lw[o >> 2], o & 3);
+}
+
+// A record header a real capture could hold: microseconds < 1e6, 0 < incl_len <= snaplen,
+// incl_len <= orig_len <= 1 MiB, and the record ends inside the file.  Only a heuristic for the
+// guess; the repair rounds make the result exact whatever it accepts.
+struct RecHdr {
+    uint32_t sec, usec, incl, orig;
+};
+
+__device__ __forceinline__ bool plausible(const RecHdr& h, uint64_t pos, uint64_t len, uint32_t snap) {
+    return h.usec < 1000000u && h.incl != 0 && h.incl <= snap && h.incl <= h.orig && h.orig <= (1u << 20) &&
+           pos + 16 + h.incl <= len;
+}
+
+__device__ __forceinline__ RecHdr hdr_lds(const uint32_t* lw, uint32_t o) {
+    return RecHdr{ld32(lw, o), ld32(lw, o + 4), ld32(lw, o + 8), ld32(lw, o + 12)};
+}
+
+// The same header read from global memory (past the staged bytes): aligned dwords below `len`
+// only, then v_alignbyte.
+__device__ __forceinline__ RecHdr hdr_global(const uint8_t* buf, uint64_t pos, uint64_t len) {
+    const uint64_t a = pos & ~3ull;
+    const uint32_t sh = (uint32_t)(pos & 3);
+    uint32_t d[5];
+#pragma unroll
+    for (int i = 0; i < 5; i++) d[i] = a + 4 * i < len ? *reinterpret_cast<const uint32_t*>(buf + a + 4 * i) : 0u;
+    return RecHdr{__builtin_amdgcn_alignbyte(d[1], d[0], sh), __builtin_amdgcn_alignbyte(d[2], d[1], sh),
+                  __builtin_amdgcn_alignbyte(d[3], d[2], sh), __builtin_amdgcn_alignbyte(d[4], d[3], sh)};
+}
+
+// A guess candidate: plausible headers chained from `c` to the end of the region (at most
+// kMaxHops checked) and at least kMinHops of them unless the file ends first; consecutive ts_sec
+// within a day.  `lbase` = file offset of LDS byte 0, `lend` = end of the staged bytes.
+// LOCAL: stop at the first hop past the staged bytes and return 2 ("needs global reads");
+// otherwise read such hops from global memory.  1 = plausible chain, 0 = not.
+template <bool LOCAL>
+__device__ __forceinline__ int chain_ok(const uint32_t* lw, const uint8_t* buf, uint64_t lbase, uint64_t lend,
+                                        uint64_t c, uint64_t stop, uint64_t len, uint32_t snap) {
+    uint64_t p = c;
+    uint32_t prev = 0;
+    for (int hops = 0; (p < stop || hops < kMinHops) && hops < kMaxHops; hops++) {
+        if (p + 16 > len) return 1;
+        if (LOCAL && p >= lend) return 2;
+        const RecHdr h = p < lend ? hdr_lds(lw, (uint32_t)(p - lbase)) : hdr_global(buf, p, len);
+        if (!plausible(h, p, len, snap)) return 0;
+        if (hops && h.sec - prev + kTsSpan > 2 * kTsSpan) return 0;
+        prev = h.sec;
+        p += 16 + (uint64_t)h.incl;
+    }
+    return 1;
+}
+
+// The nearest region left of k that claims a record start (entry inside it), or region 0.
+__device__ __forceinline__ uint32_t left_of(const Scratch& S, uint32_t k) {
+    uint32_t j = k - 1;
+    for (int s = 0; s < kLookback && j > 0 && S.entry[j] >= (uint64_t)(j + 1) * kRegion; s++) j--;
+    return j;
+}
+
+// Stage file bytes [base, base + BYTES + 16) into LDS, zeros past the file's 16-byte-rounded end,
+// plus 16 zero bytes of pad; NT threads, this one is `t`.  All loads are issued before the first
+// LDS write (one memory latency per stage, not one per piece).
+template <uint32_t BYTES, uint32_t NT>
+__device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t base, uint64_t len, uint32_t t) {
+    constexpr uint32_t kPieces = BYTES / 16 + 2, kPer = (kPieces + NT - 1) / NT;
+    uint4 v[kPer];
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++) {
+        const uint32_t q = t + i * NT;
+        const uint64_t a = base + 16ull * q;
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (q <= BYTES / 16 && a < len) v[i] = *reinterpret_cast<const uint4*>(buf + a);
+    }
+#pragma unroll
+    for (uint32_t i = 0; i < kPer; i++)
+        if (t + i * NT < kPieces) l4[t + i * NT] = v[i];
+}
+
+// Walk the records from `entry` while they start inside the region [base, base + kRegion) and
+// 16 header bytes remain: pkt_pcap_index's loop restated per region.  Every lane walks (LDS
+// broadcast reads at `lbase`-relative offsets); lane 0 writes each record's region offset to
+// `list`.
+__device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_t* list, uint64_t base,
+                                     uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err) {
+    uint64_t pos = entry;
+    cnt = 0;
+    err = 0;
+    const uint64_t end = base + kRegion;
+    const bool l0 = lane_id() == 0;
+    while (pos < end && pos + 16 <= len) {
+        const uint32_t incl = ld32(lw, (uint32_t)(pos - lbase) + 8);
+        if (pos + 16 + (uint64_t)incl > len) {  // pkt_pcap_index: record runs past the end
+            err = 1;
+            pos = len;
+            break;
+        }
+        if (l0) list[cnt] = (uint16_t)(pos - base);
+        cnt++;
+        pos += 16 + (uint64_t)incl;
+    }
+    exit = pos;
+}
+
+// Write a walked region back: the list (coalesced from LDS) and the region's words.
+__device__ __forceinline__ void store_region(const Scratch& S, uint32_t k, const uint16_t* list,
+                                             uint64_t entry, uint64_t exit, uint32_t cnt, uint32_t err) {
+    const uint32_t lane = lane_id();
+    for (uint32_t i = lane; i < cnt; i += 64) S.list[(uint64_t)k * kMaxRec + i] = list[i];
+    if (lane == 0) {
+        S.entry[k] = entry;
+        S.exit[k] = exit;
+        S.cnt[k] = cnt;
+        S.err[k] = err;
+    }
+}
+
+__global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len,
+                                                         uint32_t K, Scratch S) {
+    __shared__ uint4 lds[kBlockBytes / 16 + 2];
+    __shared__ uint16_t lst[kWaves][kMaxRec];
+    const uint32_t w = threadIdx.x / 64, lane = lane_id();
+    const uint32_t k = blockIdx.x * kWaves + w;
+    const uint64_t lbase = (uint64_t)blockIdx.x * kBlockBytes, lend = lbase + kBlockBytes;
+    stage<kBlockBytes, 256>(lds, buf, lbase, len, threadIdx.x);
+    __syncthreads();
+    if (k >= K) return;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
+    uint16_t* list = lst[w];
+    const uint64_t base = (uint64_t)k * kRegion;
+    uint64_t entry = 24;
+    if (k == 0) {
+        if (lane == 0) S.ctl[0] = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
+    } else {
+        // snaplen (global header bytes 16..19) bounds a plausible incl_len
+        uint32_t snap = *reinterpret_cast<const uint32_t*>(buf + 16);
+        if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
+        const uint64_t stop = len < base + kRegion ? len : base + kRegion;
+        entry = base + kRegion;  // none found: guess "no record starts here"
+        for (uint64_t c0 = base; c0 < stop; c0 += 64) {
+            // The lowest candidate whose chain checks out inside the staged bytes wins; only when
+            // there is none do the candidates whose chains leave them read global memory.
+            const uint64_t c = c0 + lane;
+            const int r = c < stop && c + 16 <= len ? chain_ok<true>(lw, buf, lbase, lend, c, stop, len, snap) : 0;
+            uint64_t m = __ballot(r == 1);
+            if (!m) m = __ballot(r == 2 && chain_ok<false>(lw, buf, lbase, lend, c, stop, len, snap) == 1);
+            if (m) {
+                entry = c0 + (uint64_t)__builtin_ctzll(m);
+                break;
+            }
+        }
+    }
+    uint64_t exit;
+    uint32_t cnt, err;
+    walk(lw, lbase, list, base, entry, len, exit, cnt, err);
+    wave_lds_sync();
+    store_region(S, k, list, entry, exit, cnt, err);
+}
+
+// One repair round (see the file header).  `slot` = this round's two control words.
+__global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restrict__ buf, uint64_t len,
+                                                          uint32_t K, Scratch S, uint32_t slot) {
+    __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
+    __shared__ uint16_t lst[kWaves][kMaxRec];
+    __shared__ uint32_t qk[256];
+    __shared__ uint64_t qe[256];
+    __shared__ uint32_t qn;
+    const uint32_t t = threadIdx.x, w = t / 64;
+    if (t == 0) qn = 0;
+    __syncthreads();
+    const uint32_t k = blockIdx.x * 256 + t;
+    if (k > 0 && k < K) {
+        const uint32_t j = left_of(S, k);
+        const uint64_t e = S.exit[j];
+        if (e != S.entry[k]) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[slot]), 1ull);
+            atomicMax(reinterpret_cast<unsigned long long*>(&S.ctl[slot + 1]), (unsigned long long)(K - k));
+            if ((j == 0 || S.exit[left_of(S, j)] == S.entry[j]) && e >= (uint64_t)k * kRegion) {
+                const uint32_t q = atomicAdd(&qn, 1u);
+                qk[q] = k;
+                qe[q] = e;
+            }
+        }
+    }
+    __syncthreads();
+    const uint32_t n = qn;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds[w]);
+    for (uint32_t i = w; i < n; i += kWaves) {
+        uint32_t r = qk[i];
+        uint64_t e = qe[i];
+        for (int step = 0; step < kChaseMax; step++) {
+            const uint64_t base = (uint64_t)r * kRegion;
+            wave_lds_sync();
+            if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane_id());
+            wave_lds_sync();
+            uint64_t exit;
+            uint32_t cnt, err;
+            walk(lw, base, lst[w], base, e, len, exit, cnt, err);
+            wave_lds_sync();
+            store_region(S, r, lst[w], e, exit, cnt, err);
+            e = exit;
+            if (++r >= K || e == S.entry[r] || e < (uint64_t)r * kRegion) break;
+        }
+    }
+}
+
+// Exclusive prefix of cnt within each block of kScanBlock regions (256 threads x 4), the block
+// totals to bpre, and the OR of the regions' error flags.  The last block to finish (ticket in
+// ctl[slot + 2]) then scans the block totals in place and writes the record total to
+// ctl[slot + 1]; ctl[slot] collects the error flags.
+__global__ __launch_bounds__(256) void pcap_scan_kernel(uint32_t K, uint32_t nb, Scratch S, uint32_t slot) {
+    __shared__ uint64_t wsum[4];
+    __shared__ uint64_t carry;
+    __shared__ uint32_t last;
+    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const uint32_t k0 = blockIdx.x * kScanBlock + t * 4;
+    uint32_t c[4], e = 0, s = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        c[i] = k0 + i < K ? S.cnt[k0 + i] : 0;
+        e |= k0 + i < K ? S.err[k0 + i] : 0;
+        s += c[i];
+    }
+    if (__ballot(e != 0) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.ctl[slot]), 1ull);
+    uint32_t x = s;  // inclusive wave scan
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) wsum[w] = x;
+    __syncthreads();
+    uint32_t wbase = 0;
+    for (uint32_t i = 0; i < w; i++) wbase += (uint32_t)wsum[i];
+    uint32_t run = wbase + x - s;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+        if (k0 + i < K) S.pre[k0 + i] = run;
+        run += c[i];
+    }
+    if (t == 255) S.bpre[blockIdx.x] = (uint64_t)wbase + x;
+    __threadfence();
+    __syncthreads();
+    if (t == 0) last = atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[slot + 2]), 1ull) == nb - 1;
+    __syncthreads();
+    if (!last) return;
+    // Last block: exclusive scan of the block totals (read past L1: other blocks wrote them).
+    __threadfence();
+    if (t == 0) carry = 0;
+    __syncthreads();
+    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
+        const uint32_t b = b0 + t;
+        const uint64_t v = b < nb ? __hip_atomic_load(&S.bpre[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+        uint64_t y = v;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t z = __shfl_up(y, d, 64);
+            if (lane >= (uint32_t)d) y += z;
+        }
+        __syncthreads();
+        if (lane == 63) wsum[w] = y;
+        __syncthreads();
+        uint64_t wb = carry;
+        for (uint32_t i = 0; i < w; i++) wb += wsum[i];
+        if (b < nb) S.bpre[b] = wb + y - v;
+        __syncthreads();
+        if (t == 255) carry = wb + y;
+        __syncthreads();
+    }
+    if (t == 0) S.ctl[slot + 1] = carry;
+}
+
+// 256 threads write the records of kEmitRegions consecutive regions, one record per thread per
+// step, contiguous in the output (coalesced), at the regions' scanned prefix.
+__global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
+                                                        uint64_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ lens) {
+    __shared__ uint32_t cpre[kEmitRegions + 1];
+    const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
+    if (t == 0) {
+        uint32_t run = 0;
+        for (uint32_t r = 0; r < kEmitRegions; r++) {
+            cpre[r] = run;
+            run += k0 + r < K ? S.cnt[k0 + r] : 0;
+        }
+        cpre[kEmitRegions] = run;
+    }
+    __syncthreads();
+    const uint64_t first = (uint64_t)S.pre[k0] + S.bpre[k0 / kScanBlock];
+    const uint32_t total = cpre[kEmitRegions];
+    for (uint32_t i = t; i < total; i += 256) {
+        const uint64_t idx = first + i;
+        if (idx >= cap) break;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t b = kEmitRegions / 2; b; b >>= 1)
+            if (cpre[r + b] <= i) r += b;
+        const uint32_t k = k0 + r, li = i - cpre[r], c = cpre[r + 1] - cpre[r];
+        const uint64_t base = (uint64_t)k * kRegion;
+        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
+        const uint64_t pos = base + list[li];
+        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.exit[k];
+        offsets[idx] = pos + 16;
+        lens[idx] = (uint32_t)(next - pos - 16);
+    }
+}
+
+}  // namespace
+
+extern "C" {
+int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                          uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!ctx || !buf || !n_out || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    *n_out = 0;
+    if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
+    if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
+    const uint64_t K64 = (len + kRegion - 1) / kRegion;
+    if (K64 > (1ull << 31)) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
+    const uint32_t K = (uint32_t)K64, nb = (K + kScanBlock - 1) / kScanBlock;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+
+    // Scratch: the control words, per-region words and record lists, the scan-block prefixes.
+    const uint64_t need = 8ull * kCtlWords + (uint64_t)K * (8 + 8 + 4 + 4 + 4 + 2 * kMaxRec) + 8ull * nb + 64;
+    PcapScratch& pc = ctx->pc;
+    if (pc.bytes < need) {
+        if (pc.buf) {
+            (void)hipStreamSynchronize(s);
+            (void)hipFree(pc.buf);
+            pc.buf = nullptr;
+            pc.bytes = 0;
+        }
+        e = hipMalloc(&pc.buf, need + need / 4);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
+        pc.bytes = need + need / 4;
+    }
+    if (!pc.ctl) {
+        e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kCtlWords, hipHostMallocDefault);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc (pcap index)");
+    }
+    Scratch S;
+    char* p = static_cast<char*>(pc.buf);
+    S.ctl = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * kCtlWords;
+    S.entry = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * K;
+    S.exit = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * K;
+    S.bpre = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * nb;
+    S.cnt = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * K;
+    S.err = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * K;
+    S.pre = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * K;
+    S.list = reinterpret_cast<uint16_t*>(p);
+
+    const dim3 blk(256);
+    e = hipMemsetAsync(S.ctl, 0, 8ull * kCtlWords, s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
+    hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
+    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap guess launch");
+    // Each pass: two repair rounds, then the scan and the emit on speculation, and ONE read-back.
+    // When the second round found no region disagreeing, the state it saw was the fixed point and
+    // the emitted index is final; otherwise the pass repeats (every round fixes at least the
+    // first wrong region, so K passes always suffice).
+    for (uint32_t pass = 0;; pass++) {
+        if (pass > K) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap index did not converge");
+        const uint32_t slot = 8 + 8 * (pass % kPassSlots);
+        if (pass && pass % kPassSlots == 0) {
+            e = hipMemsetAsync(S.ctl + 8, 0, 8ull * (kCtlWords - 8), s);
+            if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
+        }
+        for (uint32_t r = 0; r < 2; r++)
+            hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r);
+        hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4);
+        if (cap)
+            hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap,
+                               S, offsets, lens);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
+        e = hipMemcpyAsync(pc.ctl, S.ctl, 8ull * (slot + 8), hipMemcpyDeviceToHost, s);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
+        if (!pc.ctl[0]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
+        if (pc.ctl[slot + 2] == 0) {
+            if (pc.ctl[slot + 4]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
+            *n_out = pc.ctl[slot + 5];
+            return PKT_SUCCESS;
+        }
+    }
+}
+
+}  // extern "C"

@@ -312,6 +312,27 @@ class Parser:
                                                     self._stream(stream)), "pkt_ipv4_checksum_batch")
         return out
 
+    def pcap_index(self, buf, cap=None, stream=None):
+        """pkt_pcap_index_device: (offsets uint64, lens uint32) device tensors of the records of a
+        tests/pcap.rs-format file held in the uint8 device tensor `buf` (16-byte aligned).
+        With cap=None the count is found first and exactly that many records are written."""
+        torch = _torch()
+        assert buf.dtype == torch.uint8 and buf.is_cuda and buf.is_contiguous()
+        n = ctypes.c_uint64()
+        s = self._stream(stream)
+        if cap is None:
+            self._check(self._L.pkt_pcap_index_device(self._ctx, buf.data_ptr(), buf.numel(), None, None,
+                                                      0, ctypes.byref(n), s), "pkt_pcap_index_device")
+            cap = n.value
+        offs = torch.empty(cap, dtype=torch.uint64, device=self.torch_device)
+        lens = torch.empty(cap, dtype=torch.uint32, device=self.torch_device)
+        self._check(self._L.pkt_pcap_index_device(self._ctx, buf.data_ptr(), buf.numel(),
+                                                  offs.data_ptr() if cap else None,
+                                                  lens.data_ptr() if cap else None, cap,
+                                                  ctypes.byref(n), s), "pkt_pcap_index_device")
+        k = min(cap, n.value)
+        return offs[:k], lens[:k], n.value
+
 
 def pcap_index(buf):
     """(offsets uint64, lens uint32) of a tests/pcap.rs-format buffer, via the C ABI."""

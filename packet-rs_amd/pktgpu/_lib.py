@@ -79,6 +79,8 @@ SIGNATURES = {
     "pkt_ipv4_checksum_batch": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, _P, _P]),
     "pkt_pcap_index": (ctypes.c_int, [_P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_pcap_index_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
+                                             ctypes.POINTER(ctypes.c_uint64), _P]),
     "pkt_ipv4_checksum_host": (ctypes.c_uint16, [ctypes.c_char_p, ctypes.c_size_t]),
 }
 

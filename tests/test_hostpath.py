@@ -107,3 +107,31 @@ def test_pinned_indexed_zero_copy(P):
     # mixed: pinned slab, pageable columns -> the staged pipeline, same results
     g = P.parse_host(h, offsets=ho, lens=hl, columns="all", chunk=9999)
     check(g, oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8), "pinned slab only")
+
+
+@pytest.mark.parametrize("staging", [1, 2])
+def test_pinned_async_parse_batch(P, staging):
+    """pkt_parse_batch on pinned host buffers (no pkt_parse_host): the kernel reads the slab and
+    writes the columns over the link, asynchronously on the caller's stream."""
+    import torch
+    buf, offs, lens = gen.gen_c4(30000, seed=12)
+    n = len(offs)
+    h, ho, hl = (P.host_empty(a.shape, a.dtype) for a in (buf, offs, lens))
+    h[:], ho[:], hl[:] = buf, offs, lens
+    out = {c: P.host_empty(schema.column_shape(c, n), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
+    for c in out:
+        out[c][...] = 0
+    b = P._lib.PktBatch()
+    b.slab, b.slab_len = h.ctypes.data, h.size
+    b.offsets, b.lens, b.n = ho.ctypes.data, hl.ctypes.data, n
+    o = P._lib.PktOut()
+    for c, a in out.items():
+        setattr(o, c, a.ctypes.data if a.size else None)
+    s = torch.cuda.Stream()
+    P.set_staging(staging)
+    try:
+        P.launch(b, 0, o, stream=s)
+        s.synchronize()
+    finally:
+        P.set_staging(0)
+    check(out, oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8), f"async staging={staging}")

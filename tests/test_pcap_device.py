@@ -1,0 +1,145 @@
+"""Device pcap indexer (pkt_pcap_index_device, §8(f) row 1) against the host indexer restated in
+gen.pcap_index_py (pinned by the golden ref22.pcap, test_abi/test_oracle): identical records,
+counts, cap behaviour and errors — on the golden capture, C4 replays, and captures built to
+defeat the speculative guess (fake record chains inside payloads, zero payloads, records larger
+than a 4 KiB region, zero-length records) so the exact fix-up rounds are what makes it right.
+Ends with the whole device path: file in HBM -> device index -> indexed parse == oracle."""
+import os
+import struct
+
+import numpy as np
+import pytest
+
+import oracle
+from pktgpu import gen, schema
+
+pytestmark = pytest.mark.gpu
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture(scope="module")
+def P():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible")
+    import pktgpu
+    return pktgpu.Parser(0)
+
+
+def dev(buf):
+    import torch
+    return torch.from_numpy(np.frombuffer(bytes(buf), np.uint8).copy()).cuda()
+
+
+def check_index(P, buf, label):
+    o_ref, l_ref = gen.pcap_index_py(bytes(buf))
+    offs, lens, n = P.pcap_index(dev(buf))
+    assert n == len(o_ref), (label, n, len(o_ref))
+    assert np.array_equal(offs.cpu().numpy(), o_ref), label
+    assert np.array_equal(lens.cpu().numpy(), l_ref), label
+
+
+def records(payloads, ts=None, snap_trunc=None):
+    out = bytearray(gen.PCAP_GLOBAL_HEADER)
+    for i, p in enumerate(payloads):
+        sec, usec = (ts[i] if ts else (0, 0))
+        orig = len(p) + (snap_trunc[i] if snap_trunc else 0)
+        out += struct.pack("<IIII", sec, usec, len(p), orig) + bytes(p)
+    return bytes(out)
+
+
+def test_ref22_golden(P):
+    check_index(P, open(os.path.join(GOLD, "ref22.pcap"), "rb").read(), "ref22")
+
+
+@pytest.mark.parametrize("n", [1, 19, 20000, 300000])
+def test_c4_replay(P, n):
+    buf, offs, lens = gen.gen_c4(n, seed=100 + n)
+    o, l, m = P.pcap_index(dev(buf))
+    assert m == n
+    assert np.array_equal(o.cpu().numpy(), offs) and np.array_equal(l.cpu().numpy(), lens)
+
+
+def test_header_only_and_tails(P):
+    check_index(P, gen.PCAP_GLOBAL_HEADER, "empty capture")
+    base = records([b"\x01" * 60, b"\x02" * 70])
+    for extra in range(0, 16):  # a trailing partial record header is ignored
+        check_index(P, base + b"\x07" * extra, f"tail {extra}")
+
+
+def test_errors_match_host(P):
+    import pktgpu
+    good = records([b"\x01" * 60, b"\x02" * 70, b"\x03" * 80])
+    for bad in (good[:-3], b"\x00" * 40, b"\xd4\xc3\xb2", good[:24 + 16 + 60 + 16 + 5]):
+        with pytest.raises(ValueError):
+            pktgpu.pcap_index(bad)
+        with pytest.raises(RuntimeError):
+            P.pcap_index(dev(bad))
+
+
+def test_cap_smaller_than_count(P):
+    import torch
+    buf, offs, lens = gen.gen_c4(5000, seed=7)
+    o, l, n = P.pcap_index(dev(buf), cap=1234)
+    assert n == 5000 and o.numel() == 1234
+    assert np.array_equal(o.cpu().numpy(), offs[:1234]) and np.array_equal(l.cpu().numpy(), lens[:1234])
+    o, l, n = P.pcap_index(dev(buf), cap=0)
+    assert n == 5000 and o.numel() == 0
+
+
+def test_fake_chains_in_payloads(P):
+    """Every payload is itself a run of plausible record headers (a pcap inside the pcap), so a
+    region that starts inside a payload guesses the fake chain; the fix-up must recover."""
+    rng = np.random.default_rng(3)
+    pays = []
+    for i in range(3000):
+        inner = bytearray()
+        for _ in range(int(rng.integers(1, 6))):
+            L = int(rng.integers(1, 40))
+            inner += struct.pack("<IIII", 1, 2, L, L) + rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        pays.append(bytes(inner))
+    check_index(P, records(pays), "nested fake chains")
+
+
+def test_zero_payloads_large_and_empty_records(P):
+    rng = np.random.default_rng(4)
+    pays = []
+    for i in range(4000):
+        r = rng.random()
+        if r < 0.05:
+            pays.append(b"")                               # incl_len 0 (never "plausible")
+        elif r < 0.10:
+            pays.append(bytes(int(rng.integers(4096, 65536))))  # spans several regions, all zeros
+        elif r < 0.15:
+            pays.append(rng.integers(0, 256, int(rng.integers(5000, 20000)), dtype=np.uint8).tobytes())
+        else:
+            pays.append(bytes(int(rng.integers(1, 300))))
+    ts = [(int(rng.integers(0, 2**31)), int(rng.integers(0, 2**32))) for _ in pays]  # some usec >= 1e6
+    check_index(P, records(pays, ts=ts, snap_trunc=[int(x) for x in rng.integers(0, 3, len(pays))]),
+                "zero/large/empty")
+
+
+def test_random_captures(P):
+    rng = np.random.default_rng(5)
+    for trial in range(6):
+        n = int(rng.integers(1, 3000))
+        hi = [20, 200, 1600, 9000, 70000, 16][trial]
+        pays = [rng.integers(0, 256, int(rng.integers(0, hi)), dtype=np.uint8).tobytes() for _ in range(n)]
+        check_index(P, records(pays), f"random {trial}")
+
+
+def test_device_index_then_parse(P):
+    """Capture in HBM -> device index -> indexed parse, every column == oracle."""
+    buf, offs, lens = gen.gen_c4(60000, seed=21)
+    d = dev(buf)
+    o, l, n = P.pcap_index(d)
+    g = P.parse(d, offsets=o, lens=l, columns="all")
+    ref = oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8)
+    for k, ov in ref.items():
+        gv = g[k].cpu().numpy()
+        if k in ("hdr_type", "hdr_off"):
+            valid = np.arange(schema.MAX_HDRS)[:, None] < ref["n_hdrs"].astype(np.int64)[None, :]
+            assert not (valid & (gv != ov)).any(), k
+        else:
+            assert np.array_equal(gv, ov), k
