@@ -44,7 +44,7 @@ constexpr uint32_t kScanBlock = 1024;             // regions per first-level sca
 constexpr uint32_t kEmitRegions = 16;             // regions per emit block
 constexpr int kLookback = 64;                     // empty regions skipped when finding an entry
 constexpr int kChaseMax = 256;                    // regions one repair chase may rewrite
-constexpr int kMinHops = 3, kMaxHops = 8;         // guess chain length
+constexpr int kMinHops = 3, kMaxHops = 4;         // guess chain length
 constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec within a day
 constexpr uint32_t kPassSlots = 64;               // passes with their own control words
 
@@ -94,7 +94,11 @@ __device__ __forceinline__ bool plausible(const RecHdr& h, uint64_t pos, uint64_
 }
 
 __device__ __forceinline__ RecHdr hdr_lds(const uint32_t* lw, uint32_t o) {
-    return RecHdr{ld32(lw, o), ld32(lw, o + 4), ld32(lw, o + 8), ld32(lw, o + 12)};
+    // five dwords in one go (ds_read2 x3, one wait), then v_alignbyte
+    const uint32_t* q = lw + (o >> 2);
+    const uint32_t sh = o & 3, d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+    return RecHdr{__builtin_amdgcn_alignbyte(d1, d0, sh), __builtin_amdgcn_alignbyte(d2, d1, sh),
+                  __builtin_amdgcn_alignbyte(d3, d2, sh), __builtin_amdgcn_alignbyte(d4, d3, sh)};
 }
 
 // The same header read from global memory (past the staged bytes): aligned dwords below `len`
@@ -111,24 +115,44 @@ __device__ __forceinline__ RecHdr hdr_global(const uint8_t* buf, uint64_t pos, u
 
 // A guess candidate: plausible headers chained from `c` to the end of the region (at most
 // kMaxHops checked) and at least kMinHops of them unless the file ends first; consecutive ts_sec
-// within a day.  `lbase` = file offset of LDS byte 0, `lend` = end of the staged bytes.
-// LOCAL: stop at the first hop past the staged bytes and return 2 ("needs global reads");
-// otherwise read such hops from global memory.  1 = plausible chain, 0 = not.
-template <bool LOCAL>
-__device__ __forceinline__ int chain_ok(const uint32_t* lw, const uint8_t* buf, uint64_t lbase, uint64_t lend,
-                                        uint64_t c, uint64_t stop, uint64_t len, uint32_t snap) {
+// within a day.  chain_local checks the hops inside the staged bytes with 32-bit offsets from
+// LDS byte 0 (`lim` = file bytes from there, clamped to 32 bits) and returns 2 at the first hop
+// past them ("needs global reads"); chain_global re-checks such a candidate reading those hops
+// from global memory.  1 = plausible chain, 0 = not.
+__device__ __forceinline__ bool plausible32(const RecHdr& h, uint32_t p, uint32_t lim, uint32_t snap) {
+    // incl <= orig <= 1 MiB keeps p + 16 + incl far below 2^32 (p < 2^22 on every hop)
+    // non-short-circuit: no branch between the loads and the verdict
+    return (h.usec < 1000000u) & (h.incl != 0) & (h.incl <= snap) & (h.incl <= h.orig) & (h.orig <= (1u << 20)) &
+           (p + 16 + h.incl <= lim);
+}
+
+__device__ __forceinline__ int chain_local(const uint32_t* lw, uint32_t c, uint32_t stop, uint32_t lend, uint32_t lim,
+                                           uint32_t snap) {
+    uint32_t p = c, prev = 0;
+    for (int hops = 0; (p < stop || hops < kMinHops) && hops < kMaxHops; hops++) {
+        if (p + 16 > lim) return 1;
+        if (p >= lend) return 2;
+        const RecHdr h = hdr_lds(lw, p);
+        if (!plausible32(h, p, lim, snap) | ((hops != 0) & (h.sec - prev + kTsSpan > 2 * kTsSpan))) return 0;
+        prev = h.sec;
+        p += 16 + h.incl;
+    }
+    return 1;
+}
+
+__device__ __forceinline__ bool chain_global(const uint32_t* lw, const uint8_t* buf, uint64_t lbase, uint64_t lend,
+                                             uint64_t c, uint64_t stop, uint64_t len, uint32_t snap) {
     uint64_t p = c;
     uint32_t prev = 0;
     for (int hops = 0; (p < stop || hops < kMinHops) && hops < kMaxHops; hops++) {
-        if (p + 16 > len) return 1;
-        if (LOCAL && p >= lend) return 2;
+        if (p + 16 > len) return true;
         const RecHdr h = p < lend ? hdr_lds(lw, (uint32_t)(p - lbase)) : hdr_global(buf, p, len);
-        if (!plausible(h, p, len, snap)) return 0;
-        if (hops && h.sec - prev + kTsSpan > 2 * kTsSpan) return 0;
+        if (!plausible(h, p, len, snap)) return false;
+        if (hops && h.sec - prev + kTsSpan > 2 * kTsSpan) return false;
         prev = h.sec;
         p += 16 + (uint64_t)h.incl;
     }
-    return 1;
+    return true;
 }
 
 // The nearest region left of k that claims a record start (entry inside it), or region 0.
@@ -160,7 +184,7 @@ __device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t ba
 // Walk the records from `entry` while they start inside the region [base, base + kRegion) and
 // 16 header bytes remain: pkt_pcap_index's loop restated per region.  Every lane walks (LDS
 // broadcast reads at `lbase`-relative offsets); lane 0 writes each record's region offset to
-// `list`.
+// `list`.  (Measured: moving the walk to SGPRs, or to 32-bit offsets, was slower on MI355X.)
 __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_t* list, uint64_t base,
                                      uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err) {
     uint64_t pos = entry;
@@ -209,30 +233,38 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     uint16_t* list = lst[w];
     const uint64_t base = (uint64_t)k * kRegion;
     uint64_t entry = 24;
+#ifndef PKTGPU_PCAP_EXP
+#define PKTGPU_PCAP_EXP 0  // timing experiments only (2: stage only, 1: no walk); 0 = the product
+#endif
     if (k == 0) {
         if (lane == 0) S.ctl[0] = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
+    } else if (PKTGPU_PCAP_EXP == 2) {
+        entry = base + (lw[(base - lbase) / 4 + lane] == 0x12345678u);
     } else {
         // snaplen (global header bytes 16..19) bounds a plausible incl_len
         uint32_t snap = *reinterpret_cast<const uint32_t*>(buf + 16);
         if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
         const uint64_t stop = len < base + kRegion ? len : base + kRegion;
+        const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
         entry = base + kRegion;  // none found: guess "no record starts here"
         for (uint64_t c0 = base; c0 < stop; c0 += 64) {
             // The lowest candidate whose chain checks out inside the staged bytes wins; only when
             // there is none do the candidates whose chains leave them read global memory.
             const uint64_t c = c0 + lane;
-            const int r = c < stop && c + 16 <= len ? chain_ok<true>(lw, buf, lbase, lend, c, stop, len, snap) : 0;
+            const int r = c < stop && c + 16 <= len
+                              ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), kBlockBytes, lim, snap)
+                              : 0;
             uint64_t m = __ballot(r == 1);
-            if (!m) m = __ballot(r == 2 && chain_ok<false>(lw, buf, lbase, lend, c, stop, len, snap) == 1);
+            if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
             if (m) {
                 entry = c0 + (uint64_t)__builtin_ctzll(m);
                 break;
             }
         }
     }
-    uint64_t exit;
-    uint32_t cnt, err;
-    walk(lw, lbase, list, base, entry, len, exit, cnt, err);
+    uint64_t exit = entry;
+    uint32_t cnt = 0, err = 0;
+    if (PKTGPU_PCAP_EXP == 0) walk(lw, lbase, list, base, entry, len, exit, cnt, err);
     wave_lds_sync();
     store_region(S, k, list, entry, exit, cnt, err);
 }

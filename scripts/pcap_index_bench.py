@@ -17,6 +17,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--no-check", action="store_true", help="timing experiments on broken variants")
     a = ap.parse_args()
     import torch
     import pktgpu
@@ -33,13 +34,14 @@ def main():
     def dev_call():
         rc = L.pkt_pcap_index_device(P._ctx, d.data_ptr(), d.numel(), o.data_ptr(), l.data_ptr(), a.records,
                                      ctypes.byref(n), s)
-        assert rc == 0, rc
+        assert rc == 0 or a.no_check, rc
 
     for _ in range(3):
         dev_call()
     torch.cuda.synchronize()
-    assert n.value == a.records
-    assert np.array_equal(o.cpu().numpy(), offs) and np.array_equal(l.cpu().numpy(), lens)
+    if not a.no_check:
+        assert n.value == a.records
+        assert np.array_equal(o.cpu().numpy(), offs) and np.array_equal(l.cpu().numpy(), lens)
     t = []
     for _ in range(a.reps):
         t0 = time.perf_counter()

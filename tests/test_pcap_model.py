@@ -19,7 +19,7 @@ def u32(b, o):
 
 
 MIN_HOPS = 3
-MAX_HOPS = 8
+MAX_HOPS = 4
 CHASE_MAX = 256
 ORIG_MAX = 1 << 20
 TS_SPAN = 86400
