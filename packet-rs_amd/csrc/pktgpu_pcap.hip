@@ -233,13 +233,8 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     uint16_t* list = lst[w];
     const uint64_t base = (uint64_t)k * kRegion;
     uint64_t entry = 24;
-#ifndef PKTGPU_PCAP_EXP
-#define PKTGPU_PCAP_EXP 0  // timing experiments only (2: stage only, 1: no walk); 0 = the product
-#endif
     if (k == 0) {
         if (lane == 0) S.ctl[0] = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
-    } else if (PKTGPU_PCAP_EXP == 2) {
-        entry = base + (lw[(base - lbase) / 4 + lane] == 0x12345678u);
     } else {
         // snaplen (global header bytes 16..19) bounds a plausible incl_len
         uint32_t snap = *reinterpret_cast<const uint32_t*>(buf + 16);
@@ -262,9 +257,9 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             }
         }
     }
-    uint64_t exit = entry;
-    uint32_t cnt = 0, err = 0;
-    if (PKTGPU_PCAP_EXP == 0) walk(lw, lbase, list, base, entry, len, exit, cnt, err);
+    uint64_t exit;
+    uint32_t cnt, err;
+    walk(lw, lbase, list, base, entry, len, exit, cnt, err);
     wave_lds_sync();
     store_region(S, k, list, entry, exit, cnt, err);
 }
@@ -389,13 +384,16 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
                                                         uint32_t* __restrict__ lens) {
     __shared__ uint32_t cpre[kEmitRegions + 1];
     const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
-    if (t == 0) {
-        uint32_t run = 0;
-        for (uint32_t r = 0; r < kEmitRegions; r++) {
-            cpre[r] = run;
-            run += k0 + r < K ? S.cnt[k0 + r] : 0;
+    if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
+        const uint32_t c = t < kEmitRegions && k0 + t < K ? S.cnt[k0 + t] : 0;
+        uint32_t x = c;
+#pragma unroll
+        for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (t >= d) x += y;
         }
-        cpre[kEmitRegions] = run;
+        if (t < kEmitRegions) cpre[t] = x - c;
+        if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
     }
     __syncthreads();
     const uint64_t first = (uint64_t)S.pre[k0] + S.bpre[k0 / kScanBlock];
