@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PKTGPU_ABI_VERSION 1
+#define PKTGPU_ABI_VERSION 2
 
 /* Maximum number of headers recorded per packet.  The reference recursion is unbounded
  * (fast.rs:53 VLAN stacks, :69 MPLS stacks, :89/:92/:104/:107 IP-in-IP, :168/:186/:219
@@ -367,6 +367,67 @@ int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint
 
 /* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
 uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
+
+/* ---- packed output buffers (host only, no device needed) ----
+ * A column mask selects pkt_out_t members: bit k = the k-th pointer of pkt_out_t (0 = status,
+ * ..., 48 = udp_checksum).  The packed layout puts every selected column of an n-packet output in
+ * one buffer, in pkt_out_t order, each column starting on a 256-byte boundary (slot columns are
+ * [PKT_MAX_HDRS][n]).  One buffer per shard is what the multi-GPU gather moves in one message. */
+#define PKT_COL(k)      (1ull << (k))
+#define PKT_COLS_ALL    ((1ull << 49) - 1)
+#define PKT_COLS_CHAIN  0x7Full               /* status .. hdr_mask */
+#define PKT_COLS_ETHER  (0x7ull << 7)
+#define PKT_COLS_VLAN   (0xFull << 10)
+#define PKT_COLS_IPV4   (0x1FFFull << 14)
+#define PKT_COLS_IPV6   (0xFFull << 27)
+#define PKT_COLS_TCP    (0x3FFull << 35)
+#define PKT_COLS_UDP    (0xFull << 45)
+/* Fills `out` with the selected columns' pointers inside `base` (NULL columns elsewhere; `base`
+ * may be NULL to size only) and sets *bytes to the buffer size. */
+int pkt_out_packed(uint64_t col_mask, uint64_t n, void *base, pkt_out_t *out, uint64_t *bytes);
+/* The column mask of a pkt_out_t (bit k set iff its k-th pointer is non-NULL). */
+uint64_t pkt_out_mask(const pkt_out_t *out);
+/* [lo, hi) of shard i of n packets split into `nshards` contiguous blocks whose sizes differ by
+ * at most one (the lower shards take the remainder). */
+int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t *lo, uint64_t *hi);
+
+/* ---- multi-GPU: one process drives several devices ----
+ * Every fast::parse_* is a pure function of one packet (fast.rs:5-227), so a batch splits into
+ * contiguous shards, one per device, with no exchange inside the parse.  The only collective is
+ * the gather of the per-packet tuples to a root device over RCCL (xGMI): one grouped
+ * ncclSend / ncclRecv per shard (ncclCommInitAll over the device list; one communicator per
+ * device, owned by the handle).  Each device has its own pkt_ctx and work stream; every call
+ * below is asynchronous on those streams and returns after the launches (pkt_mgpu_synchronize
+ * waits).  One host thread at a time per handle. */
+typedef struct pkt_mgpu pkt_mgpu_t;
+/* `devices`: ndev distinct HIP device ids; index 0..ndev-1 into this list is the "shard" id. */
+int         pkt_mgpu_create(const int *devices, int ndev, pkt_mgpu_t **mg);
+int         pkt_mgpu_destroy(pkt_mgpu_t *mg);
+int         pkt_mgpu_ndev(const pkt_mgpu_t *mg);
+const char *pkt_mgpu_last_error(const pkt_mgpu_t *mg);
+/* The per-device ctx (tuning knobs, other batched calls) and work stream (a hipStream_t). */
+pkt_ctx_t  *pkt_mgpu_ctx(pkt_mgpu_t *mg, int shard);
+void       *pkt_mgpu_stream(pkt_mgpu_t *mg, int shard);
+/* Parse shard i: batches[i] (resident on devices[i]) -> the packed output buffer shard_out[i]
+ * (device memory of devices[i], pkt_out_packed(col_mask, batches[i].n) bytes). */
+int pkt_mgpu_parse(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
+                   void *const *shard_out);
+/* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
+ * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.
+ * Grouped ncclSend/ncclRecv (the root's own block is a send to itself). */
+int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uint64_t *bytes,
+                    void *recv, uint64_t recv_len, const uint64_t *recv_off);
+/* pkt_mgpu_parse, then the gather of every shard's packed tuple buffer into `recv` on the root
+ * (consecutive 256-B aligned blocks).  root_views (host array of ndev pkt_out_t, may be NULL)
+ * receives the column pointers of each shard's tuples inside `recv`.  With `merge` = 1 the
+ * tuples land as ONE packed output of sum(n) packets instead (recv = pkt_out_packed(col_mask,
+ * sum n) bytes, shards in order: what pkt_parse_batch over the whole batch would write); the
+ * gather then sends each column (each slot row) of a shard as its own message, and root_views[0]
+ * receives that single view. */
+int pkt_mgpu_parse_gather(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
+                          void *const *shard_out, int root, void *recv, uint64_t recv_len,
+                          int merge, pkt_out_t *root_views);
+int pkt_mgpu_synchronize(pkt_mgpu_t *mg);
 
 #ifdef __cplusplus
 }

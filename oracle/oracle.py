@@ -165,6 +165,28 @@ def slow_parse_to_vec(pkt, entry=0):
     return buf.raw[:k]
 
 
+def round_trip_batch(slab, n, stride=None, offsets=None, lens=None, entry=0, slow=True, nthreads=1,
+                     dst=None):
+    """Batched `parser::{slow,fast}::parse(pkt).to_vec()` (tests/lib.rs:790-817) written at each
+    packet's own position; returns (dst, out_len)."""
+    if isinstance(entry, str):
+        entry = schema.ENTRY_ID[entry]
+    b, keep = _batch(slab, n, stride, offsets, lens)
+    flat = keep[0]
+    if dst is None:
+        dst = np.zeros(flat.size, np.uint8)
+    out_len = np.zeros(n, np.uint32)
+    L = lib()
+    L.orc_round_trip_batch.restype = ctypes.c_int
+    L.orc_round_trip_batch.argtypes = [ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int]
+    rc = L.orc_round_trip_batch(ctypes.byref(b), entry, 1 if slow else 0, dst.ctypes.data, dst.size,
+                                out_len.ctypes.data, nthreads)
+    if rc != 0:
+        raise RuntimeError(f"orc_round_trip_batch failed ({rc})")
+    return dst, out_len
+
+
 def set_bit_range(hdr, msb, lsb, value):
     """headers.rs:315-324 on a bytearray (returns a new bytes)."""
     a = (ctypes.c_uint8 * len(hdr)).from_buffer_copy(bytes(hdr))

@@ -684,6 +684,75 @@ long orc_slow_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out
     return (long)k;
 }
 
+/* PacketSlice::to_vec (packet.rs:733-740) after fast::parse: the header slices in list order,
+ * then the payload — no owned copies (tests/lib.rs:804-817 parse_slice_test). */
+static long fast_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out, size_t cap) {
+    orc_pslice_t ps = {0};
+    walk_t w = {p, len, 0};
+    int st = ENTRY_FNS[entry](&w, 0, &ps);
+    if (st != PKT_OK) { ps_free(&ps); return -st; }
+    size_t k = 0;
+    for (size_t j = 0; j < ps.n; j++) {
+        size_t sz = (size_t)ORC_HDRS[ps.hdrs[j]->type].size;
+        if (k + sz <= cap) memcpy(out + k, p + ps.hdrs[j]->off, sz);
+        k += sz;
+    }
+    if (k + ps.payload_len <= cap) memcpy(out + k, p + ps.payload_off, ps.payload_len);
+    k += ps.payload_len;
+    ps_free(&ps);
+    return (long)k;
+}
+
+typedef struct {
+    const pkt_batch_t *b;
+    int entry, slow;
+    uint8_t *dst;
+    uint64_t dst_len;
+    uint32_t *out_len;
+    uint64_t lo, hi;
+} rt_job_t;
+
+static void *run_rt_job(void *arg) {
+    rt_job_t *j = (rt_job_t *)arg;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const uint8_t *p;
+        size_t len;
+        packet_bounds(j->b, i, &p, &len);
+        const uint64_t o = j->b->offsets ? j->b->offsets[i] : i * (uint64_t)j->b->stride;
+        const size_t cap = o < j->dst_len ? (size_t)(j->dst_len - o) : 0;
+        long k = j->slow ? orc_slow_parse_to_vec(p, len, j->entry, j->dst + o, cap)
+                         : fast_parse_to_vec(p, len, j->entry, j->dst + o, cap);
+        if (j->out_len) j->out_len[i] = k > 0 ? (uint32_t)k : 0;
+    }
+    return NULL;
+}
+
+/* Batched round trip, the CPU baseline of tests/lib.rs:790-817: for every packet,
+ * slow::parse(..).to_vec() (slow = 1, parse_test) or fast::parse(..).to_vec() (slow = 0,
+ * parse_slice_test), written at the packet's own position in dst (i*stride or offsets[i]).
+ * out_len[i] = bytes written (0 when the reference would panic). */
+int orc_round_trip_batch(const pkt_batch_t *b, int entry, int slow, uint8_t *dst, uint64_t dst_len,
+                         uint32_t *out_len, int nthreads) {
+    if (!b || !dst || entry < 0 || entry >= PKT_ENTRY_COUNT) return -1;
+    if (b->n && !b->slab) return -1;
+    if (b->offsets && !b->lens) return -1;
+    if (nthreads < 1) nthreads = 1;
+    if ((uint64_t)nthreads > b->n) nthreads = b->n ? (int)b->n : 1;
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    rt_job_t *jobs = (rt_job_t *)calloc((size_t)nthreads, sizeof(rt_job_t));
+    if (!th || !jobs) { free(th); free(jobs); return -1; }
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (rt_job_t){b, entry, slow, dst, dst_len, out_len, b->n * (uint64_t)t / (uint64_t)nthreads,
+                             b->n * (uint64_t)(t + 1) / (uint64_t)nthreads};
+        if (nthreads > 1) pthread_create(&th[t], NULL, run_rt_job, &jobs[t]);
+    }
+    if (nthreads == 1) run_rt_job(&jobs[0]);
+    else for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+    return 0;
+}
+
 /* ------------------------------------------------------------------ header rewrite */
 /* headers.rs:315-324 — set_bit_range: for i in (lsb..=msb).rev(): bit i := value & 1;
  * value >>= 1 (one bit at a time, with the lock-free slice here). */

@@ -23,6 +23,8 @@ int orc_set_fields(const pkt_batch_t *b, const pkt_chain_t *chain, const pkt_fie
                    uint32_t nspec, const uint64_t *const *values);
 int orc_ipv4_update_checksum(const pkt_batch_t *b, const pkt_chain_t *chain, uint32_t occurrence);
 long orc_slow_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out, size_t cap);
+int orc_round_trip_batch(const pkt_batch_t *b, int entry, int slow, uint8_t *dst, uint64_t dst_len,
+                         uint32_t *out_len, int nthreads);
 #ifdef __cplusplus
 }
 #endif

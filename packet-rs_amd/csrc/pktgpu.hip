@@ -849,12 +849,6 @@ bool host_mapped(T* p, T*& dev) {
     return true;
 }
 
-// Element size of each pkt_out_t column, in declaration order (slot columns: one slot).
-constexpr uint8_t kSize[49] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
-                               1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
-                               1, 1, 2, 2, 2, 2, 2, 2, 2};
-constexpr int kColHdrType = 2, kColHdrOff = 3;  // slot-major [PKT_MAX_HDRS][n]
-
 // Grow one device buffer of every pipeline slot to `need` bytes (all slots idle: the caller has
 // synchronised the pipeline streams).
 template <class T>
@@ -1012,7 +1006,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         for (int c = 0; c < 49; c++)
-            if (oc[c]) oc[c] += i0 * kSize[c];
+            if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
         if (nch <= 2) e = launch_gm<2>(kp, gm, mode, wk, s);
         else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, wk, s);
@@ -1113,7 +1107,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         col_off[c] = out_need;
         if (!hcol[c]) continue;
         const uint64_t rows = (c == kColHdrType || c == kColHdrOff) ? PKT_MAX_HDRS : 1;
-        out_need += (rows * cn * kSize[c] + 255) & ~(uint64_t)255;
+        out_need += (rows * cn * kColSize[c] + 255) & ~(uint64_t)255;
     }
     for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
     if ((e = grow(hp.slab, hp.slab_cap, (slab_need + 15) & ~(uint64_t)15)) != hipSuccess ||
@@ -1160,7 +1154,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         for (int c = 0; c < 49 && e == hipSuccess; c++) {
             if (!hcol[c]) continue;
             uint8_t* h = const_cast<uint8_t*>(hcol[c]);
-            const uint64_t sz = kSize[c];
+            const uint64_t sz = kColSize[c];
             if (c == kColHdrType || c == kColHdrOff)
                 e = hipMemcpy2DAsync(h + lo * sz, n * sz, dcol[c], m * sz, m * sz, PKT_MAX_HDRS,
                                      hipMemcpyDeviceToHost, s);

@@ -27,6 +27,20 @@ struct PcapScratch {
     uint64_t* ctl = nullptr;  // pinned host words the indexer reads back (change count, totals)
 };
 
+// Element size of each pkt_out_t column, in declaration order (slot columns: one slot; the
+// ipv6 addresses: 16 raw bytes).
+constexpr int kNumCols = 49;
+constexpr uint8_t kColSize[kNumCols] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2, 1, 1, 1, 2, 2, 1, 2,
+                                        1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
+                                        1, 1, 2, 2, 2, 2, 2, 2, 2};
+constexpr int kColHdrType = 2, kColHdrOff = 3;  // slot-major [PKT_MAX_HDRS][n]
+static_assert(sizeof(pkt_out_t) == kNumCols * sizeof(void*), "pkt_out_t layout");
+
+// Bytes of column c for n packets.
+inline uint64_t col_bytes(int c, uint64_t n) {
+    return n * kColSize[c] * ((c == kColHdrType || c == kColHdrOff) ? PKT_MAX_HDRS : 1);
+}
+
 struct pkt_ctx {
     int device;
     HostPipe hp;

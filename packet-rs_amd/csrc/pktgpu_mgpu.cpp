@@ -1,0 +1,270 @@
+// pktgpu_mgpu.cpp — packed output layout and the multi-GPU entry (pkt_mgpu_*) of the C ABI.
+//
+// One process drives several MI355X devices.  Every fast::parse_* is a pure function of one
+// packet's bytes (reference src/parser/fast.rs:5-227), so a batch splits into contiguous shards
+// with no exchange inside the parse; the only collective is the gather of the per-packet tuples
+// to the root device: grouped ncclSend/ncclRecv (RCCL over xGMI) on one communicator per device
+// from ncclCommInitAll.  A shard's tuples live in ONE packed buffer (pkt_out_packed), so the
+// gather is one message per shard; the merged form sends each column (slot row) separately.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "pktgpu_ctx.hpp"
+
+struct pkt_mgpu {
+    int ndev = 0;
+    std::vector<int> dev;
+    std::vector<pkt_ctx_t*> ctx;
+    std::vector<hipStream_t> stream;
+    std::vector<ncclComm_t> comm;
+    std::string err;
+};
+
+namespace {
+
+constexpr uint64_t kAlign = 256;
+inline uint64_t round_up(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
+
+int mfail(pkt_mgpu* mg, int code, const std::string& msg) {
+    if (mg) mg->err = msg;
+    return code;
+}
+int mhip(pkt_mgpu* mg, hipError_t e, const char* what) {
+    return mfail(mg, PKT_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+int mnccl(pkt_mgpu* mg, ncclResult_t r, const char* what) {
+    return mfail(mg, PKT_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
+}
+
+// Offset of column c inside a packed buffer of n packets (selected columns only, in order).
+uint64_t packed_layout(uint64_t mask, uint64_t n, uint64_t* off /* [kNumCols] or NULL */) {
+    uint64_t o = 0;
+    for (int c = 0; c < kNumCols; c++) {
+        if (!(mask >> c & 1)) continue;
+        if (off) off[c] = o;
+        o += round_up(col_bytes(c, n));
+    }
+    return o;
+}
+
+// Merged gather plan: (source offset in the shard buffer, destination offset in the root
+// buffer, bytes) of each message — one per column, one per slot row for slot columns.
+struct Piece {
+    uint64_t src, dst, bytes;
+};
+void merged_pieces(uint64_t mask, uint64_t n_i, uint64_t lo, uint64_t n_total, std::vector<Piece>& out) {
+    uint64_t so[kNumCols], dof[kNumCols];
+    packed_layout(mask, n_i, so);
+    packed_layout(mask, n_total, dof);
+    out.clear();
+    if (n_i == 0) return;
+    for (int c = 0; c < kNumCols; c++) {
+        if (!(mask >> c & 1)) continue;
+        const uint64_t esz = kColSize[c];
+        if (c == kColHdrType || c == kColHdrOff) {
+            for (uint64_t j = 0; j < PKT_MAX_HDRS; j++)
+                out.push_back({so[c] + j * n_i * esz, dof[c] + (j * n_total + lo) * esz, n_i * esz});
+        } else {
+            out.push_back({so[c], dof[c] + lo * esz, n_i * esz});
+        }
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int pkt_out_packed(uint64_t mask, uint64_t n, void* base, pkt_out_t* out, uint64_t* bytes) {
+    if (mask >> kNumCols) return PKT_ERR_INVALID_ARG;
+    uint64_t off[kNumCols];
+    const uint64_t total = packed_layout(mask, n, off);
+    if (bytes) *bytes = total;
+    if (out) {
+        void** cols = reinterpret_cast<void**>(out);
+        for (int c = 0; c < kNumCols; c++)
+            cols[c] = (base && (mask >> c & 1)) ? static_cast<uint8_t*>(base) + off[c] : nullptr;
+    }
+    return PKT_SUCCESS;
+}
+
+uint64_t pkt_out_mask(const pkt_out_t* out) {
+    if (!out) return 0;
+    const void* const* cols = reinterpret_cast<const void* const*>(out);
+    uint64_t m = 0;
+    for (int c = 0; c < kNumCols; c++)
+        if (cols[c]) m |= 1ull << c;
+    return m;
+}
+
+int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t* lo, uint64_t* hi) {
+    if (nshards <= 0 || i < 0 || i >= nshards || !lo || !hi) return PKT_ERR_INVALID_ARG;
+    const uint64_t base = n / (uint64_t)nshards, extra = n % (uint64_t)nshards;
+    *lo = (uint64_t)i * base + std::min<uint64_t>((uint64_t)i, extra);
+    *hi = *lo + base + ((uint64_t)i < extra ? 1 : 0);
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
+    if (!out || !devices || ndev <= 0) return PKT_ERR_INVALID_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return PKT_ERR_NO_DEVICE;
+    for (int i = 0; i < ndev; i++) {
+        if (devices[i] < 0 || devices[i] >= count) return PKT_ERR_INVALID_ARG;
+        for (int j = 0; j < i; j++)
+            if (devices[j] == devices[i]) return PKT_ERR_INVALID_ARG;  // one communicator per device
+    }
+    pkt_mgpu* mg = new pkt_mgpu();
+    mg->ndev = ndev;
+    mg->dev.assign(devices, devices + ndev);
+    mg->ctx.assign(ndev, nullptr);
+    mg->stream.assign(ndev, nullptr);
+    mg->comm.assign(ndev, nullptr);
+    int rc = PKT_SUCCESS;
+    for (int i = 0; i < ndev && rc == PKT_SUCCESS; i++) {
+        rc = pkt_ctx_create(devices[i], &mg->ctx[i]);
+        if (rc != PKT_SUCCESS) break;
+        hipError_t e = hipSetDevice(devices[i]);
+        if (e == hipSuccess) e = hipStreamCreateWithFlags(&mg->stream[i], hipStreamNonBlocking);
+        if (e != hipSuccess) rc = PKT_ERR_HIP;
+    }
+    if (rc == PKT_SUCCESS) {
+        ncclResult_t r = ncclCommInitAll(mg->comm.data(), ndev, mg->dev.data());
+        if (r != ncclSuccess) {
+            for (auto& c : mg->comm) c = nullptr;
+            rc = PKT_ERR_HIP;
+        }
+    }
+    if (rc != PKT_SUCCESS) {
+        pkt_mgpu_destroy(mg);
+        return rc;
+    }
+    *out = mg;
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
+    if (!mg) return PKT_SUCCESS;
+    for (int i = 0; i < mg->ndev; i++) {
+        (void)hipSetDevice(mg->dev[i]);
+        if (mg->stream[i]) (void)hipStreamSynchronize(mg->stream[i]);
+        if (mg->comm[i]) (void)ncclCommDestroy(mg->comm[i]);
+        if (mg->stream[i]) (void)hipStreamDestroy(mg->stream[i]);
+        if (mg->ctx[i]) pkt_ctx_destroy(mg->ctx[i]);
+    }
+    delete mg;
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_ndev(const pkt_mgpu_t* mg) { return mg ? mg->ndev : 0; }
+const char* pkt_mgpu_last_error(const pkt_mgpu_t* mg) { return mg ? mg->err.c_str() : "null handle"; }
+pkt_ctx_t* pkt_mgpu_ctx(pkt_mgpu_t* mg, int i) { return (mg && i >= 0 && i < mg->ndev) ? mg->ctx[i] : nullptr; }
+void* pkt_mgpu_stream(pkt_mgpu_t* mg, int i) {
+    return (mg && i >= 0 && i < mg->ndev) ? reinterpret_cast<void*>(mg->stream[i]) : nullptr;
+}
+
+int pkt_mgpu_parse(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry, uint64_t mask, void* const* shard_out) {
+    if (!mg || !batches || !shard_out) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
+    if (mask >> kNumCols) return mfail(mg, PKT_ERR_INVALID_ARG, "bad column mask");
+    for (int i = 0; i < mg->ndev; i++) {
+        if (batches[i].n && !shard_out[i]) return mfail(mg, PKT_ERR_INVALID_ARG, "null shard output");
+        pkt_out_t o;
+        pkt_out_packed(mask, batches[i].n, shard_out[i], &o, nullptr);
+        const int rc = pkt_parse_batch(mg->ctx[i], &batches[i], entry, &o, mg->stream[i]);
+        if (rc != PKT_SUCCESS)
+            return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
+    }
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_gather(pkt_mgpu_t* mg, int root, const void* const* send, const uint64_t* bytes, void* recv,
+                    uint64_t recv_len, const uint64_t* recv_off) {
+    if (!mg || !send || !bytes) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
+    if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
+    std::vector<uint64_t> off(mg->ndev);
+    uint64_t o = 0;
+    for (int i = 0; i < mg->ndev; i++) {
+        off[i] = recv_off ? recv_off[i] : o;
+        o = round_up(off[i] + bytes[i]);
+        if (bytes[i] && (!send[i] || !recv)) return mfail(mg, PKT_ERR_INVALID_ARG, "null buffer");
+        if (off[i] + bytes[i] > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
+    }
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
+    for (int i = 0; i < mg->ndev && r == ncclSuccess; i++) {
+        if (!bytes[i]) continue;
+        r = ncclSend(send[i], bytes[i], ncclUint8, root, mg->comm[i], mg->stream[i]);
+        if (r == ncclSuccess)
+            r = ncclRecv(static_cast<uint8_t*>(recv) + off[i], bytes[i], ncclUint8, i, mg->comm[root],
+                         mg->stream[root]);
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return mnccl(mg, r, "ncclSend/ncclRecv");
+    if (r2 != ncclSuccess) return mnccl(mg, r2, "ncclGroupEnd");
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry, uint64_t mask,
+                          void* const* shard_out, int root, void* recv, uint64_t recv_len, int merge,
+                          pkt_out_t* root_views) {
+    if (!mg || !batches || !shard_out) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
+    if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
+    if (merge != 0 && merge != 1) return mfail(mg, PKT_ERR_INVALID_ARG, "bad merge flag");
+    int rc = pkt_mgpu_parse(mg, batches, entry, mask, shard_out);
+    if (rc != PKT_SUCCESS) return rc;
+    const int nd = mg->ndev;
+    if (!merge) {
+        std::vector<const void*> send(nd);
+        std::vector<uint64_t> bytes(nd), off(nd);
+        uint64_t o = 0;
+        for (int i = 0; i < nd; i++) {
+            send[i] = shard_out[i];
+            bytes[i] = packed_layout(mask, batches[i].n, nullptr);
+            off[i] = o;
+            o = round_up(o + bytes[i]);
+            if (root_views) pkt_out_packed(mask, batches[i].n, static_cast<uint8_t*>(recv) + off[i], &root_views[i], nullptr);
+        }
+        return pkt_mgpu_gather(mg, root, send.data(), bytes.data(), recv, recv_len, off.data());
+    }
+    uint64_t n_total = 0;
+    for (int i = 0; i < nd; i++) n_total += batches[i].n;
+    if (packed_layout(mask, n_total, nullptr) > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
+    if (n_total && !recv) return mfail(mg, PKT_ERR_INVALID_ARG, "null recv");
+    if (root_views) pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
+    std::vector<Piece> pieces;
+    ncclResult_t r = ncclGroupStart();
+    if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
+    uint64_t lo = 0;
+    for (int i = 0; i < nd && r == ncclSuccess; i++) {
+        merged_pieces(mask, batches[i].n, lo, n_total, pieces);
+        lo += batches[i].n;
+        for (const Piece& p : pieces) {
+            r = ncclSend(static_cast<const uint8_t*>(shard_out[i]) + p.src, p.bytes, ncclUint8, root, mg->comm[i],
+                         mg->stream[i]);
+            if (r != ncclSuccess) break;
+            r = ncclRecv(static_cast<uint8_t*>(recv) + p.dst, p.bytes, ncclUint8, i, mg->comm[root], mg->stream[root]);
+            if (r != ncclSuccess) break;
+        }
+    }
+    const ncclResult_t r2 = ncclGroupEnd();
+    if (r != ncclSuccess) return mnccl(mg, r, "ncclSend/ncclRecv");
+    if (r2 != ncclSuccess) return mnccl(mg, r2, "ncclGroupEnd");
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_synchronize(pkt_mgpu_t* mg) {
+    if (!mg) return PKT_ERR_INVALID_ARG;
+    for (int i = 0; i < mg->ndev; i++) {
+        hipError_t e = hipSetDevice(mg->dev[i]);
+        if (e == hipSuccess) e = hipStreamSynchronize(mg->stream[i]);
+        if (e != hipSuccess) return mhip(mg, e, "hipStreamSynchronize");
+    }
+    return PKT_SUCCESS;
+}
+
+}  // extern "C"

@@ -1,0 +1,82 @@
+// pktgpu_probe.hip — measurement probe for bench.py (lib/libpktprobe.so; NOT part of the product
+// ABI and never called by it).
+//
+// pkt_probe_ceiling: the "ceiling" kernel of the roofline line.  Same launch shape as the C2
+// parse launch (256-thread blocks, one packet per lane, grid = n / 256) and the SAME HBM traffic
+// — each lane loads its packet's first 64 bytes with four 16-byte loads and stores the C2 bench
+// tuple (chain with 3 slots + Ether + IPv4 + UDP = 69 B) into the same pkt_out_t columns with
+// the same per-lane store widths — but no walk and no field logic: every stored value is a cheap
+// mix of the loaded words.  Its launch time is what ANY kernel with C2's traffic shape costs in
+// one launch on this box, so parse / ceiling says how much of the gap to the HBM peak is the
+// parser's own.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/pktgpu.h"
+
+namespace {
+
+template <class T>
+__device__ __forceinline__ void put(T* base, uint32_t i, T v) { base[i] = v; }
+
+__global__ __launch_bounds__(256) void ceiling_kernel(const uint8_t* slab, uint32_t n, uint32_t stride,
+                                                      pkt_out_t o) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint4* p = reinterpret_cast<const uint4*>(slab + (uint64_t)i * stride);
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    const uint32_t v0 = a.x ^ d.w, v1 = a.y ^ c.z, v2 = a.z ^ b.y, v3 = a.w ^ c.x;
+    const uint32_t v4 = b.x ^ d.x, v5 = b.z ^ c.y, v6 = b.w ^ d.y, v7 = c.w ^ d.z;
+    // chain: status, n_hdrs, 3 header slots (type, offset), payload, mask
+    put<uint8_t>(o.status, i, (uint8_t)(v0 & 1));
+    put<uint8_t>(o.n_hdrs, i, (uint8_t)(3 + (v1 & 1)));
+#pragma unroll
+    for (uint32_t j = 0; j < 3; j++) {
+        put<uint8_t>(o.hdr_type, j * n + i, (uint8_t)(v2 >> (8 * j)));
+        put<uint16_t>(o.hdr_off, j * n + i, (uint16_t)(v3 >> (5 * j)));
+    }
+    put<uint16_t>(o.payload_off, i, (uint16_t)v4);
+    put<uint16_t>(o.payload_len, i, (uint16_t)(v4 >> 16));
+    put<uint32_t>(o.hdr_mask, i, v5);
+    // Ether
+    put<uint64_t>(o.eth_dst, i, ((uint64_t)a.x << 16) | (a.y >> 16));
+    put<uint64_t>(o.eth_src, i, ((uint64_t)a.y << 32) | a.z);
+    put<uint16_t>(o.eth_etype, i, (uint16_t)a.w);
+    // IPv4
+    put<uint8_t>(o.ipv4_version, i, (uint8_t)(v6 >> 4));
+    put<uint8_t>(o.ipv4_ihl, i, (uint8_t)v6);
+    put<uint8_t>(o.ipv4_diffserv, i, (uint8_t)(v6 >> 8));
+    put<uint16_t>(o.ipv4_total_len, i, (uint16_t)(v6 >> 16));
+    put<uint16_t>(o.ipv4_identification, i, (uint16_t)v7);
+    put<uint8_t>(o.ipv4_flags, i, (uint8_t)(v7 >> 29));
+    put<uint16_t>(o.ipv4_frag_startset, i, (uint16_t)(v7 >> 16));
+    put<uint8_t>(o.ipv4_ttl, i, (uint8_t)(b.x >> 8));
+    put<uint8_t>(o.ipv4_protocol, i, (uint8_t)b.x);
+    put<uint16_t>(o.ipv4_header_checksum, i, (uint16_t)(b.y >> 16));
+    put<uint32_t>(o.ipv4_src, i, b.z);
+    put<uint32_t>(o.ipv4_dst, i, b.w);
+    put<uint16_t>(o.ipv4_csum_calc, i, (uint16_t)(v0 + v1 + v2 + v3));
+    // UDP
+    put<uint16_t>(o.udp_src, i, (uint16_t)c.x);
+    put<uint16_t>(o.udp_dst, i, (uint16_t)(c.x >> 16));
+    put<uint16_t>(o.udp_length, i, (uint16_t)c.y);
+    put<uint16_t>(o.udp_checksum, i, (uint16_t)(c.y >> 16));
+}
+
+}  // namespace
+
+extern "C" int pkt_probe_ceiling(const uint8_t* slab, uint64_t n, uint32_t stride, const pkt_out_t* out,
+                                 void* stream) {
+    // The probe stores the C2 bench set only; every one of its columns must be present.
+    if (!slab || !out || n == 0 || n >= (1ull << 26) || stride < 64 || (stride & 15)) return PKT_ERR_INVALID_ARG;
+    // pkt_out_t members 0-9 (chain, Ether), 14-26 (IPv4) and 45-48 (UDP)
+    const void* const* cols = reinterpret_cast<const void* const*>(out);
+    for (int c = 0; c < 49; c++) {
+        const bool need = c < 10 || (c >= 14 && c < 27) || c >= 45;
+        if (need && !cols[c]) return PKT_ERR_INVALID_ARG;
+    }
+    hipLaunchKernelGGL(ceiling_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), slab, (uint32_t)n, stride, *out);
+    return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
+}

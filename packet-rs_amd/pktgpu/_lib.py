@@ -82,6 +82,26 @@ SIGNATURES = {
     "pkt_pcap_index_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
                                              ctypes.POINTER(ctypes.c_uint64), _P]),
     "pkt_ipv4_checksum_host": (ctypes.c_uint16, [ctypes.c_char_p, ctypes.c_size_t]),
+    # packed outputs + multi-GPU (pkt_mgpu_*)
+    "pkt_out_packed": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, _P, ctypes.POINTER(PktOut),
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_out_mask": (ctypes.c_uint64, [ctypes.POINTER(PktOut)]),
+    "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_mgpu_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
+    "pkt_mgpu_destroy": (ctypes.c_int, [_P]),
+    "pkt_mgpu_ndev": (ctypes.c_int, [_P]),
+    "pkt_mgpu_last_error": (ctypes.c_char_p, [_P]),
+    "pkt_mgpu_ctx": (_P, [_P, ctypes.c_int]),
+    "pkt_mgpu_stream": (_P, [_P, ctypes.c_int]),
+    "pkt_mgpu_parse": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_uint64,
+                                      ctypes.POINTER(_P)]),
+    "pkt_mgpu_gather": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint64),
+                                       _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_mgpu_parse_gather": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_uint64,
+                                             ctypes.POINTER(_P), ctypes.c_int, _P, ctypes.c_uint64,
+                                             ctypes.c_int, ctypes.POINTER(PktOut)]),
+    "pkt_mgpu_synchronize": (ctypes.c_int, [_P]),
 }
 
 _lib = None

@@ -1,0 +1,198 @@
+"""One process, several devices: the pkt_mgpu_* entry of the C ABI (include/pktgpu.h).
+
+A batch splits into contiguous shards, one per device (every fast::parse_* is a pure function of
+one packet, reference src/parser/fast.rs:5-227, so no exchange is needed inside the parse).  Each
+shard's per-packet tuples are written into ONE packed device buffer (pkt_out_packed layout) and
+gathered to the root device by grouped ncclSend/ncclRecv over RCCL — one message per shard, or
+per column with merge=True (the root then holds exactly what one pkt_parse_batch over the whole
+batch would write).
+
+    >>> mp = MultiParser([0, 1, 2, 3, 4, 5, 6, 7])
+    >>> shards = mp.shard_fixed(slab_host_u8, n, stride=64)     # one device slab per GPU
+    >>> res = mp.parse_gather(shards, columns=["chain", "ipv4", "udp"], merge=True)
+    >>> res["ipv4_src"]                                          # torch tensor on devices[0]
+"""
+import ctypes
+
+import numpy as np
+
+from . import _tdtype, _torch, resolve_columns, schema
+
+
+def packed_views(buf, columns, n):
+    """{column: torch view} of an n-packet packed output buffer (uint8 device tensor), using the
+    library's own layout (pkt_out_packed)."""
+    from . import _lib
+    L = _lib.load()
+    cols = resolve_columns(columns)
+    mask = schema.column_mask(cols)
+    o = _lib.PktOut()
+    nb = ctypes.c_uint64()
+    base = buf.data_ptr()
+    rc = L.pkt_out_packed(mask, int(n), ctypes.c_void_p(base), ctypes.byref(o), ctypes.byref(nb))
+    if rc != 0:
+        raise ValueError("pkt_out_packed failed")
+    if buf.numel() < nb.value:
+        raise ValueError(f"packed buffer too small: {buf.numel()} < {nb.value}")
+    views = {}
+    for c in cols:
+        off = getattr(o, c) - base
+        shp = schema.column_shape(c, n)
+        nbytes = int(np.prod(shp)) * schema.column_dtype(c).itemsize
+        views[c] = buf[off:off + nbytes].view(_tdtype(schema.column_dtype(c))).view(shp)
+    return views
+
+
+def packed_bytes(columns, n):
+    from . import _lib
+    L = _lib.load()
+    nb = ctypes.c_uint64()
+    rc = L.pkt_out_packed(schema.column_mask(resolve_columns(columns)), int(n), None, None, ctypes.byref(nb))
+    if rc != 0:
+        raise ValueError("pkt_out_packed failed")
+    return nb.value
+
+
+def shard_range(n, nshards, i):
+    """The library's contiguous split (pkt_shard_range): [lo, hi) of shard i."""
+    from . import _lib
+    L = _lib.load()
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    if L.pkt_shard_range(int(n), int(nshards), int(i), ctypes.byref(lo), ctypes.byref(hi)) != 0:
+        raise ValueError("pkt_shard_range: bad arguments")
+    return lo.value, hi.value
+
+
+class MultiParser:
+    """A pkt_mgpu handle over a list of distinct HIP devices (one RCCL communicator each)."""
+
+    def __init__(self, devices):
+        torch = _torch()
+        from . import _lib
+        self._lib = _lib
+        self._L = _lib.load()
+        self.devices = [int(d) for d in devices]
+        self.torch_devices = [torch.device("cuda", d) for d in self.devices]
+        arr = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = ctypes.c_void_p()
+        rc = self._L.pkt_mgpu_create(arr, len(self.devices), ctypes.byref(h))
+        if rc != 0:
+            raise RuntimeError(f"pkt_mgpu_create({self.devices}) failed: {rc}")
+        self._mg = h
+
+    @property
+    def ndev(self):
+        return len(self.devices)
+
+    def close(self):
+        if getattr(self, "_mg", None):
+            self._L.pkt_mgpu_destroy(self._mg)
+            self._mg = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc, what):
+        if rc != 0:
+            msg = self._L.pkt_mgpu_last_error(self._mg)
+            raise RuntimeError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+    def ctx(self, i):
+        return self._L.pkt_mgpu_ctx(self._mg, i)
+
+    def synchronize(self):
+        self._check(self._L.pkt_mgpu_synchronize(self._mg), "pkt_mgpu_synchronize")
+
+    # ---------------------------------------------------------------- inputs
+    def shard_fixed(self, slab, n, stride, lens=None):
+        """Copy the contiguous shards of a host fixed-stride slab (numpy uint8) to the devices:
+        [(slab tensor, n_i, stride, None, lens tensor|None)]."""
+        torch = _torch()
+        slab = np.ascontiguousarray(slab, np.uint8).reshape(-1)
+        out = []
+        for i, dev in enumerate(self.torch_devices):
+            lo, hi = shard_range(n, self.ndev, i)
+            s = torch.from_numpy(slab[lo * stride:hi * stride].copy()).to(dev) if hi > lo else \
+                torch.zeros(16, dtype=torch.uint8, device=dev)
+            ln = torch.from_numpy(np.ascontiguousarray(lens[lo:hi], np.uint32)).to(dev) if lens is not None else None
+            out.append((s, hi - lo, stride, None, ln))
+        return out
+
+    def shard_indexed(self, buf, offsets, lens):
+        """Shards of an indexed (pcap) batch by record index; each device gets the whole file
+        and its records' (offsets, lens)."""
+        torch = _torch()
+        a = np.ascontiguousarray(np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
+        out = []
+        for i, dev in enumerate(self.torch_devices):
+            lo, hi = shard_range(len(offsets), self.ndev, i)
+            out.append((torch.from_numpy(a.copy()).to(dev), hi - lo, 0,
+                        torch.from_numpy(np.ascontiguousarray(offsets[lo:hi], np.uint64)).to(dev),
+                        torch.from_numpy(np.ascontiguousarray(lens[lo:hi], np.uint32)).to(dev)))
+        return out
+
+    def _batches(self, shards):
+        arr = (self._lib.PktBatch * self.ndev)()
+        for i, (slab, n, stride, offs, lens) in enumerate(shards):
+            b = arr[i]
+            b.slab = slab.data_ptr()
+            b.slab_len = slab.numel()
+            b.offsets = offs.data_ptr() if offs is not None else None
+            b.lens = lens.data_ptr() if lens is not None else None
+            b.stride = stride or 0
+            b.n = int(n)
+        return arr
+
+    # ---------------------------------------------------------------- parse + gather
+    def alloc_shard_outputs(self, shards, columns):
+        torch = _torch()
+        return [torch.empty(max(1, packed_bytes(columns, s[1])), dtype=torch.uint8, device=dev)
+                for s, dev in zip(shards, self.torch_devices)]
+
+    def parse(self, shards, entry="parse", columns="all", shard_out=None):
+        """Parse every shard on its device -> [packed buffer per shard] (asynchronous)."""
+        e = schema.ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        cols = resolve_columns(columns)
+        if shard_out is None:
+            shard_out = self.alloc_shard_outputs(shards, cols)
+        ptrs = (ctypes.c_void_p * self.ndev)(*[b.data_ptr() for b in shard_out])
+        self._check(self._L.pkt_mgpu_parse(self._mg, self._batches(shards), e, schema.column_mask(cols), ptrs),
+                    "pkt_mgpu_parse")
+        return shard_out
+
+    def recv_bytes(self, shards, columns, merge):
+        cols = resolve_columns(columns)
+        if merge:
+            return packed_bytes(cols, sum(s[1] for s in shards))
+        return sum((packed_bytes(cols, s[1]) + 255) // 256 * 256 for s in shards)
+
+    def parse_gather(self, shards, entry="parse", columns="all", root=0, merge=False,
+                     shard_out=None, recv=None):
+        """Parse + RCCL gather into one device buffer on devices[root].  Returns (views, recv,
+        shard_out): views = one {column: tensor} for merge=True (the whole batch), else one per
+        shard.  Asynchronous on the handle's streams; call synchronize() before reading."""
+        torch = _torch()
+        e = schema.ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        cols = resolve_columns(columns)
+        mask = schema.column_mask(cols)
+        if shard_out is None:
+            shard_out = self.alloc_shard_outputs(shards, cols)
+        need = self.recv_bytes(shards, cols, merge)
+        if recv is None:
+            recv = torch.empty(max(1, need), dtype=torch.uint8, device=self.torch_devices[root])
+        ptrs = (ctypes.c_void_p * self.ndev)(*[b.data_ptr() for b in shard_out])
+        views = (self._lib.PktOut * self.ndev)()
+        self._check(self._L.pkt_mgpu_parse_gather(self._mg, self._batches(shards), e, mask, ptrs, root,
+                                                  ctypes.c_void_p(recv.data_ptr()), recv.numel(),
+                                                  1 if merge else 0, views), "pkt_mgpu_parse_gather")
+        if merge:
+            return packed_views(recv, cols, sum(s[1] for s in shards)), recv, shard_out
+        out, o = [], 0
+        for s in shards:
+            nb = packed_bytes(cols, s[1])
+            out.append(packed_views(recv[o:o + max(nb, 1)], cols, s[1]) if s[1] else {})
+            o += (nb + 255) // 256 * 256
+        return out, recv, shard_out

@@ -8,7 +8,7 @@ change without bumping PKTGPU_ABI_VERSION.
 import numpy as np
 
 MAX_HDRS = 16
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # pkt_status_t
 OK, TRUNCATED, DEPTH_LIMIT = 0, 1, 2
@@ -112,6 +112,12 @@ def column_dtype(name):
         if c == name:
             return np.dtype(dt)
     raise KeyError(name)
+
+
+def column_mask(columns):
+    """pkt_out_t column mask (bit k = k-th member) of a set of column names."""
+    cols = set(columns)
+    return sum(1 << k for k, c in enumerate(COLUMN_NAMES) if c in cols)
 
 
 def bytes_per_packet(columns, n_slots=MAX_HDRS):

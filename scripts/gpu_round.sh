@@ -31,14 +31,14 @@ if [ $rc -ne 0 ]; then exit $rc; fi
 
 echo "== rocprofv3 kernel trace (one stream: per-dispatch durations = the roofline phase)"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o trace -- \
-    python bench.py --steps 50 --warmup 5 --no-cpu-baseline --streams 1 "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+    python bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-c5 --streams 1 "$@" > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 rc=$?; echo "rocprof rc=$rc"; tail -2 "$OUT/prof.err"
 if [ $rc -ne 0 ]; then exit $rc; fi
 echo "== PMC traffic passes"
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o pmc -- \
-    python bench.py --steps 20 --warmup 2 --no-cpu-baseline --streams 1 "$@" > /dev/null 2>&1 && \
+    python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c5 --streams 1 "$@" > /dev/null 2>&1 && \
 timeout -k 10 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o pmc -- \
-    python bench.py --steps 20 --warmup 2 --no-cpu-baseline --streams 1 "$@" > /dev/null 2>&1 && \
+    python bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-c5 --streams 1 "$@" > /dev/null 2>&1 && \
 python scripts/traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/traffic.json" parse_kernel "$TAG $*"
 rc=$?; echo "pmc rc=$rc"
 exit $rc

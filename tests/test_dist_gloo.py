@@ -1,7 +1,8 @@
-"""world_size-2 gloo tests (CPU) of the multi-GPU path: contiguous sharding (even, uneven and
+"""world_size-2 gloo tests of the multi-GPU path: contiguous sharding (even, uneven and
 pcap-indexed), per-rank parse, and the tuple gather reassembled in global order must equal the
-single-process parse of the whole batch.  The per-rank compute here is the oracle (no GPU);
-on GPUs the same code runs with pktgpu.Parser and the nccl (RCCL) backend."""
+single-process parse of the whole batch.  CPU variant: the per-rank compute is the oracle (no
+GPU here).  GPU variant (-m gpu): each rank parses its shard with the HIP path (pktgpu.Parser;
+both ranks share the box's one device) and the gathered tuples are checked against the oracle."""
 import os
 import socket
 import sys
@@ -21,7 +22,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, case, q):
+def _worker(rank, world, port, case, q, use_gpu=False):
     sys.path[:0] = [os.path.join(REPO, "packet-rs_amd"), os.path.join(REPO, "oracle")]
     import torch.distributed as dist
     import oracle
@@ -36,11 +37,17 @@ def _worker(rank, world, port, case, q):
             slab = gen.gen_c3(n, seed=21)
             flat = slab.reshape(-1)
             view, nl, _, lo = pd.shard_fixed(flat, n, 128, world, rank)
-            res = oracle.parse_batch(view, nl, stride=128, columns=cols)
+            if use_gpu:
+                res = _gpu_parse(np.ascontiguousarray(view), nl, 128, None, None, cols)
+            else:
+                res = oracle.parse_batch(view, nl, stride=128, columns=cols)
         else:
             buf, offs, lens = gen.gen_c4(3001, seed=22)
             o, l, lo = pd.shard_indexed(offs, lens, world, rank)
-            res = oracle.parse_batch(buf, len(o), offsets=o, lens=l, columns=cols)
+            if use_gpu:
+                res = _gpu_parse(buf, len(o), None, o, l, cols)
+            else:
+                res = oracle.parse_batch(buf, len(o), offsets=o, lens=l, columns=cols)
             nl = len(o)
         merged = pd.gather_columns(res, cols, nl, dst=0)
         if rank == 0:
@@ -63,18 +70,41 @@ def _worker(rank, world, port, case, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("case", ["even", "uneven", "pcap"])
-def test_sharded_parse_and_gather_world2(case):
+def _gpu_parse(slab, n, stride, offs, lens, cols):
+    """This rank's shard through the HIP path; columns come back as CPU tensors (gloo)."""
+    import torch
+    import pktgpu
+    P = pktgpu.Parser(0)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a)).cuda()  # noqa: E731
+    res = P.parse(d(np.frombuffer(slab, np.uint8) if isinstance(slab, bytes) else slab.reshape(-1)),
+                  stride=stride, n=n, offsets=d(offs.astype(np.uint64)) if offs is not None else None,
+                  lens=d(lens.astype(np.uint32)) if lens is not None else None, columns=cols)
+    torch.cuda.synchronize()
+    return {k: v.cpu() for k, v in res.items()}
+
+
+def _run(case, use_gpu):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, case, q, use_gpu)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert q.get(timeout=10) == []
+
+
+@pytest.mark.parametrize("case", ["even", "uneven", "pcap"])
+def test_sharded_parse_and_gather_world2(case):
+    _run(case, use_gpu=False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", ["uneven", "pcap"])
+def test_sharded_hip_parse_and_gather_world2(case):
+    _run(case, use_gpu=True)
 
 
 def test_shard_range_partition():

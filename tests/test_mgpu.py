@@ -1,0 +1,147 @@
+"""The multi-GPU entry of the C ABI (pkt_mgpu_*, pkt_out_packed, pkt_shard_range).
+
+CPU tests: the packed layout and the shard split are host-only functions of the library; they
+are checked against the Python schema and pktgpu.dist's split.  GPU tests: one process drives
+the box's devices through pkt_mgpu (ncclCommInitAll + grouped ncclSend/ncclRecv; a 1-GPU box
+gives ndev = 1, where the root's block is an RCCL send to itself) and the gathered tuples must
+equal the oracle's over the whole batch — fast::parse is a pure function of each packet
+(reference src/parser/fast.rs:5-12), so sharding must not change a single byte.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+import oracle
+from pktgpu import _lib, dist, gen, schema
+
+
+def _L():
+    return _lib.load()
+
+
+def test_packed_layout_matches_schema():
+    L = _L()
+    rng = np.random.default_rng(3)
+    for trial in range(60):
+        cols = [c for c in schema.COLUMN_NAMES if rng.random() < 0.5] or ["status"]
+        n = int(rng.integers(0, 5000))
+        mask = schema.column_mask(cols)
+        o = _lib.PktOut()
+        nb = ctypes.c_uint64()
+        base = 1 << 20
+        assert L.pkt_out_packed(mask, n, ctypes.c_void_p(base), ctypes.byref(o), ctypes.byref(nb)) == 0
+        off = 0
+        for c in schema.COLUMN_NAMES:
+            p = getattr(o, c)
+            if c not in cols:
+                assert p is None, c
+                continue
+            assert p == base + off, (c, p - base, off)
+            sz = int(np.prod(schema.column_shape(c, n))) * schema.column_dtype(c).itemsize
+            off += (sz + 255) // 256 * 256
+        assert nb.value == off
+        assert L.pkt_out_mask(ctypes.byref(o)) == mask
+    assert L.pkt_out_packed(1 << 49, 10, None, None, ctypes.byref(nb)) != 0
+
+
+def test_shard_range_matches_dist():
+    L = _L()
+    lo, hi = ctypes.c_uint64(), ctypes.c_uint64()
+    for n in (0, 1, 7, 8, 9, 1 << 20, (1 << 24) + 3):
+        for k in (1, 2, 3, 4, 7, 8):
+            prev = 0
+            for i in range(k):
+                assert L.pkt_shard_range(n, k, i, ctypes.byref(lo), ctypes.byref(hi)) == 0
+                assert (lo.value, hi.value) == dist.shard_range(n, k, i)
+                assert lo.value == prev
+                prev = hi.value
+            assert prev == n
+    assert L.pkt_shard_range(10, 0, 0, ctypes.byref(lo), ctypes.byref(hi)) != 0
+    assert L.pkt_shard_range(10, 2, 2, ctypes.byref(lo), ctypes.byref(hi)) != 0
+
+
+def test_mgpu_create_rejects_bad_device_lists():
+    L = _L()
+    h = ctypes.c_void_p()
+    assert L.pkt_mgpu_create(None, 1, ctypes.byref(h)) != 0
+    arr = (ctypes.c_int * 1)(0)
+    assert L.pkt_mgpu_create(arr, 0, ctypes.byref(h)) != 0
+    arr2 = (ctypes.c_int * 2)(0, 0)
+    assert L.pkt_mgpu_create(arr2, 2, ctypes.byref(h)) != 0  # duplicate device (or no device)
+    assert not h.value
+
+
+# ------------------------------------------------------------------------------------------ GPU
+def _compare(g, o, label):
+    for k, ov in o.items():
+        gv = g[k].cpu().numpy() if hasattr(g[k], "cpu") else g[k]
+        if k in ("hdr_type", "hdr_off"):
+            valid = np.arange(schema.MAX_HDRS)[:, None] < o["n_hdrs"].astype(np.int64)[None, :]
+            assert not (valid & (gv != ov)).any(), f"{label} {k}"
+        else:
+            assert np.array_equal(gv, ov), f"{label} {k}"
+
+
+@pytest.fixture(scope="module")
+def MP():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible: -m gpu tests need an MI355X")
+    from pktgpu.mgpu import MultiParser
+    return MultiParser(list(range(torch.cuda.device_count())))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("merge", [False, True])
+def test_mgpu_c2_parse_gather_vs_oracle(MP, merge):
+    n = 100_003
+    slab = gen.gen_c2(n, seed=77)
+    cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+    shards = MP.shard_fixed(slab, n, 64)
+    views, recv, _ = MP.parse_gather(shards, columns=cols, merge=merge)
+    MP.synchronize()
+    o = oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8)
+    if merge:
+        _compare(views, o, "merged")
+    else:
+        assert len(views) == MP.ndev
+        merged = {}
+        for c in cols:
+            parts = [v[c].cpu().numpy() for v in views if v]
+            merged[c] = np.concatenate(parts, axis=1 if c in ("hdr_type", "hdr_off") else 0)
+        _compare(merged, o, "per-shard")
+
+
+@pytest.mark.gpu
+def test_mgpu_c4_pcap_all_columns_vs_oracle(MP):
+    n = 20_000
+    buf, offs, lens = gen.gen_c4(n, seed=41)
+    shards = MP.shard_indexed(buf, offs, lens)
+    views, _, _ = MP.parse_gather(shards, columns="all", merge=True)
+    MP.synchronize()
+    o = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    _compare(views, o, "c4 merged")
+
+
+@pytest.mark.gpu
+def test_mgpu_parse_only_and_entries(MP):
+    """pkt_mgpu_parse alone (no gather) into the packed shard buffers, a non-default entry."""
+    from pktgpu.mgpu import packed_views
+    n = 4099
+    rng = np.random.default_rng(5)
+    slab = rng.integers(0, 256, n * 48, dtype=np.uint8)
+    cols = schema.columns_of(["chain", "ipv4", "udp"])
+    shards = MP.shard_fixed(slab, n, 48)
+    bufs = MP.parse(shards, entry="parse_ipv4", columns=cols)
+    MP.synchronize()
+    o = oracle.parse_batch(slab, n, stride=48, entry="parse_ipv4", columns=cols, nthreads=8)
+    lo = 0
+    for (s, ni, *_), b in zip(shards, bufs):
+        if not ni:
+            continue
+        v = packed_views(b, cols, ni)
+        sub = {k: (val[:, lo:lo + ni] if k in ("hdr_type", "hdr_off") else val[lo:lo + ni]) for k, val in o.items()}
+        _compare(v, sub, "parse_ipv4 shard")
+        lo += ni
+    assert lo == n
