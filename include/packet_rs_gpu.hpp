@@ -14,6 +14,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -117,6 +118,10 @@ struct BatchResult {
 };
 
 // A pkt_ctx plus device scratch for the chain columns.
+struct DeviceFree {
+    void operator()(void* p) const { (void)hipFree(p); }
+};
+
 class Parser {
    public:
     explicit Parser(int device = 0) { check(pkt_ctx_create(device, &ctx_), nullptr, "pkt_ctx_create"); }
@@ -134,6 +139,8 @@ class Parser {
         void* d = nullptr;
         const size_t bytes = n * (1 + 1 + PKT_MAX_HDRS + 2 * PKT_MAX_HDRS + 2 + 2 + 4) + 64;
         hip_check(hipMalloc(&d, bytes), "hipMalloc");
+        // freed on every exit, including a hip_check throw below
+        std::unique_ptr<void, DeviceFree> guard(d);
         uint8_t* base = static_cast<uint8_t*>(d);
         pkt_out_t o;
         std::memset(&o, 0, sizeof(o));
@@ -165,7 +172,6 @@ class Parser {
             hip_check(hipMemcpy(r.payload_len.data(), o.payload_len, 2 * n, hipMemcpyDeviceToHost), "copy");
             hip_check(hipMemcpy(r.hdr_mask.data(), o.hdr_mask, 4 * n, hipMemcpyDeviceToHost), "copy");
         }
-        (void)hipFree(d);
         check(rc, ctx_, "pkt_parse_batch");
         return r;
     }

@@ -47,7 +47,8 @@ __device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
 }
 
 // Fields of the first header of each group (Q11), from the walk's first offsets.
-// `i` is the packet index within this launch (< 2^28, so every byte offset fits 32 bits).
+// `i` is the packet index within this launch (< kLaunchChunk = 2^26, so every per-packet byte
+// offset, up to i * 16 for the IPv6 addresses, fits 32 bits).
 template <uint32_t GM, class View>
 __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, const View& pv,
                                             const WalkResult& r, bool ok) {
@@ -986,9 +987,8 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
-    const uint64_t kChunk = 1ull << 26;  // packets per launch (32-bit byte offsets in-kernel)
-    for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kChunk) {
-        const uint64_t cnt = std::min<uint64_t>(kChunk, b->n - i0);
+    for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kLaunchChunk) {
+        const uint64_t cnt = std::min<uint64_t>(kLaunchChunk, b->n - i0);
         KParams kp;
         kp.slab = b->slab;
         kp.slab_len = b->slab_len;

@@ -39,9 +39,12 @@ enum State : uint32_t {
 // pkt_entry_t -> first state (entries 1..17 map 1:1 onto S_DOT3..S_VXLAN)
 __device__ __forceinline__ uint32_t entry_state(int entry) { return (uint32_t)entry; }
 
-// One launch covers packets [i0, i0 + n) of a batch (n < 2^28 so that every per-packet byte
-// offset fits 32 bits); offsets/lens/per-packet columns are pre-offset by i0 on the host, the
-// slot-major hdr_type/hdr_off columns are pre-offset by i0 and strided by the batch size.
+// One launch covers packets [i0, i0 + n) of a batch, n <= kLaunchChunk, so that every per-packet
+// column byte offset (at most i * 16, the IPv6 addresses) fits 32 bits; offsets/lens/per-packet
+// columns are pre-offset by i0 on the host, the slot-major hdr_type/hdr_off columns are pre-offset
+// by i0 and strided by the batch size (64-bit offsets).
+constexpr uint64_t kLaunchChunk = 1ull << 26;
+static_assert(kLaunchChunk * 16 <= (1ull << 32), "per-packet column offsets must fit 32 bits");
 struct KParams {
     const uint8_t* slab;
     uint64_t slab_len;

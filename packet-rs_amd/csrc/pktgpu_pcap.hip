@@ -22,7 +22,11 @@
 //           Every region left of the first disagreement is exact (region 0 is, and each agrees
 //           with an exact left), so the first queued chase is exact and no round ends without
 //           fixing at least that region; a round in which no region disagrees is the exact fixed
-//           point — the true chain, whatever the guesses were.
+//           point — the true chain, whatever the guesses were.  A chase claims each region before
+//           rewriting it (atomicMax of the round id on the region's owner word) and stops at a
+//           region another chase already claimed this round, so a region's entry, exit, count,
+//           error and list always come from ONE walk; the first queued chase cannot be stopped
+//           (chases only move right and start at queued regions), which keeps the progress bound.
 //   SCAN    exclusive prefix of the per-region counts (per 1024 regions; the last block to finish
 //           scans the block totals).
 //   EMIT    256 threads write 16 regions' records at their prefix: offset = pos + 16, incl_len =
@@ -62,6 +66,7 @@ struct Scratch {
     uint32_t* pre;     // exclusive prefix of cnt within its scan block
     uint64_t* bpre;    // exclusive prefix of the scan blocks
     uint16_t* list;    // [region][kMaxRec] record offsets relative to the region base
+    uint32_t* own;     // the last repair round whose chase rewrote the region (0 = none)
     uint64_t* ctl;     // control words above
 };
 
@@ -266,7 +271,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
 
 // One repair round (see the file header).  `slot` = this round's two control words.
 __global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restrict__ buf, uint64_t len,
-                                                          uint32_t K, Scratch S, uint32_t slot) {
+                                                          uint32_t K, Scratch S, uint32_t slot, uint32_t round) {
     __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
     __shared__ uint16_t lst[kWaves][kMaxRec];
     __shared__ uint32_t qk[256];
@@ -296,6 +301,10 @@ __global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restr
         uint32_t r = qk[i];
         uint64_t e = qe[i];
         for (int step = 0; step < kChaseMax; step++) {
+            // claim region r for this round; a region another chase claimed first is its alone
+            uint32_t prev = 0;
+            if (lane_id() == 0) prev = atomicMax(&S.own[r], round);
+            if (__shfl(prev, 0, 64) >= round) break;
             const uint64_t base = (uint64_t)r * kRegion;
             wave_lds_sync();
             if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane_id());
@@ -432,7 +441,7 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
     // Scratch: the control words, per-region words and record lists, the scan-block prefixes.
-    const uint64_t need = 8ull * kCtlWords + (uint64_t)K * (8 + 8 + 4 + 4 + 4 + 2 * kMaxRec) + 8ull * nb + 64;
+    const uint64_t need = 8ull * kCtlWords + (uint64_t)K * (8 + 8 + 4 + 4 + 4 + 4 + 2 * kMaxRec) + 8ull * nb + 64;
     PcapScratch& pc = ctx->pc;
     if (pc.bytes < need) {
         if (pc.buf) {
@@ -465,10 +474,13 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     p += 4ull * K;
     S.pre = reinterpret_cast<uint32_t*>(p);
     p += 4ull * K;
+    S.own = reinterpret_cast<uint32_t*>(p);
+    p += 4ull * K;
     S.list = reinterpret_cast<uint16_t*>(p);
 
     const dim3 blk(256);
     e = hipMemsetAsync(S.ctl, 0, 8ull * kCtlWords, s);
+    if (e == hipSuccess) e = hipMemsetAsync(S.own, 0, 4ull * K, s);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
     hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap guess launch");
@@ -483,8 +495,9 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
             e = hipMemsetAsync(S.ctl + 8, 0, 8ull * (kCtlWords - 8), s);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
         }
-        for (uint32_t r = 0; r < 2; r++)
-            hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r);
+        for (uint32_t r = 0; r < 2; r++)  // round ids 1, 2, 3, ... (owner words start at 0)
+            hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r,
+                               2 * pass + r + 1);
         hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4);
         if (cap)
             hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap,

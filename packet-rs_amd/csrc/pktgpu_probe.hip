@@ -80,3 +80,33 @@ extern "C" int pkt_probe_ceiling(const uint8_t* slab, uint64_t n, uint32_t strid
                        reinterpret_cast<hipStream_t>(stream), slab, (uint32_t)n, stride, *out);
     return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
 }
+
+// pkt_probe_fetch: FETCH_SIZE calibration for per-lane scattered reads (the access shape of the
+// indexed-batch windows).  Item i (one lane) reads `width` bytes (16-byte loads) at
+// buf + i * stride + phase and writes one word, so with stride >= 256 every item touches its own
+// lines: FETCH_SIZE per item says at which granularity (64-B sector or 128-B line) the memory-side
+// requests of this shape are counted.
+namespace {
+__global__ __launch_bounds__(256) void fetch_kernel(const uint8_t* buf, uint32_t n, uint32_t stride, uint32_t phase,
+                                                    uint32_t width, uint32_t* out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint4* p = reinterpret_cast<const uint4*>(buf + (uint64_t)i * stride + phase);
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < width / 16; c++) {
+        const uint4 v = p[c];
+        acc ^= v.x + v.y * 3u + v.z * 5u + v.w * 7u;
+    }
+    out[i] = acc;
+}
+}  // namespace
+
+extern "C" int pkt_probe_fetch(const uint8_t* buf, uint64_t buf_len, uint32_t n, uint32_t stride, uint32_t phase,
+                               uint32_t width, uint32_t* out, void* stream) {
+    if (!buf || !out || !n || (phase & 15) || (width & 15) || width == 0 ||
+        (uint64_t)(n - 1) * stride + phase + width > buf_len)
+        return PKT_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(fetch_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), buf,
+                       n, stride, phase, width, out);
+    return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
+}

@@ -142,10 +142,16 @@ def test_c3_full_1m(P):
     assert set(np.unique(g["n_hdrs"])) == {3, 4, 5}
 
 
-def test_c4_pcap(P):
-    n = 1 << 16
+@pytest.mark.parametrize("staging", [0, 2])
+def test_c4_pcap(P, staging):
+    """Config 4 at its bench size: 2^20 pcap records of the 22 templates, every column."""
+    n = 1 << 20
     buf, offs, lens = gen.gen_c4(n, seed=4)
-    both(P, buf, n, offsets=offs, lens=lens, label="c4")
+    P.set_staging(staging)
+    try:
+        both(P, buf, n, offsets=offs, lens=lens, label=f"c4 staging={staging}")
+    finally:
+        P.set_staging(0)
 
 
 def test_c2_chain_only_and_subsets(P):

@@ -53,7 +53,7 @@ def test_ref22_golden(P):
     check_index(P, open(os.path.join(GOLD, "ref22.pcap"), "rb").read(), "ref22")
 
 
-@pytest.mark.parametrize("n", [1, 19, 20000, 300000])
+@pytest.mark.parametrize("n", [1, 19, 20000, 300000, 1 << 20])
 def test_c4_replay(P, n):
     buf, offs, lens = gen.gen_c4(n, seed=100 + n)
     o, l, m = P.pcap_index(dev(buf))
@@ -130,8 +130,9 @@ def test_random_captures(P):
 
 
 def test_device_index_then_parse(P):
-    """Capture in HBM -> device index -> indexed parse, every column == oracle."""
-    buf, offs, lens = gen.gen_c4(60000, seed=21)
+    """Capture in HBM -> device index -> indexed parse, every column == oracle, at C4's bench
+    size (2^20 records, tests/pcap.rs:7-37 format)."""
+    buf, offs, lens = gen.gen_c4(1 << 20, seed=21)
     d = dev(buf)
     o, l, n = P.pcap_index(d)
     g = P.parse(d, offsets=o, lens=l, columns="all")

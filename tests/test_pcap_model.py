@@ -82,11 +82,19 @@ def guess(b, k, snap):
     return base + R
 
 
-def model_index(b):
+def model_index(b, inject=None, order_seed=None):
+    """`inject` {region: entry} overrides the guess (adversarial wrong guesses); `order_seed`
+    runs each round's chases in a random order instead of queue order.  A chase claims every
+    region it rewrites for the round and stops at one another chase claimed first (the owner
+    words of pcap_repair_kernel), so each region's words come from one walk."""
     b = bytes(b)
     snap = u32(b, 16) or (1 << 30)
     K = (len(b) + R - 1) // R
     entry = [24 if k == 0 else guess(b, k, snap) for k in range(K)]
+    for k, e in (inject or {}).items():
+        if 0 < k < K:
+            entry[k] = e
+    rng = np.random.default_rng(order_seed) if order_seed is not None else None
     state = [walk(b, k * R, entry[k]) for k in range(K)]
     rounds = 0
     while True:
@@ -112,8 +120,14 @@ def model_index(b):
             # and then chases on through the following regions until an exit meets a stored entry
             if (j == 0 or old_state[left(j)][0] == old_entry[j]) and e >= k * R:
                 queue.append((k, e))
-        for k, e in queue:  # one interleaving of the chasing waves: in queue order
+        if rng is not None:
+            queue = [queue[i] for i in rng.permutation(len(queue))]
+        owned = set()
+        for k, e in queue:  # one interleaving of the chasing waves
             for _ in range(CHASE_MAX):
+                if k in owned:  # claimed by another chase this round
+                    break
+                owned.add(k)
                 entry[k] = e
                 state[k] = walk(b, k * R, e)
                 e = state[k][0]
@@ -142,9 +156,9 @@ def records(pays, ts=None):
     return bytes(out)
 
 
-def check(b):
+def check(b, **kw):
     o1, l1 = gen.pcap_index_py(b)
-    o2, l2, rounds = model_index(b)
+    o2, l2, rounds = model_index(b, **kw)
     assert np.array_equal(o1, o2) and np.array_equal(l1, l2)
     return rounds
 
@@ -185,3 +199,21 @@ def test_model_errors_and_tails():
         raise AssertionError("expected an error")
     except ValueError:
         pass
+
+
+def test_model_adjacent_wrong_guesses_any_chase_order():
+    """Wrong guesses in regions a and a+2 (and runs of them), chases in random orders: the
+    ownership rule keeps every region consistent and the fixed point exact."""
+    buf, _, _ = gen.gen_c4(3000, seed=11)
+    b = buf.tobytes()
+    K = (len(b) + R - 1) // R
+    rng = np.random.default_rng(12)
+    for trial in range(40):
+        a = int(rng.integers(1, K - 6))
+        bad = {a: a * R + int(rng.integers(0, R)), a + 2: (a + 2) * R + int(rng.integers(0, R))}
+        if trial % 3 == 0:  # a run of wrong guesses
+            for k in range(a + 3, min(K, a + 3 + int(rng.integers(1, 6)))):
+                bad[k] = k * R + int(rng.integers(0, R))
+        if trial % 4 == 1:  # a wrong guess pointing into the next region
+            bad[a + 1] = (a + 2) * R + 17
+        check(b, inject=bad, order_seed=trial)
