@@ -344,6 +344,53 @@ int pkt_ipv4_update_checksum(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt
 int pkt_broadcast(pkt_ctx_t *ctx, const uint8_t *src, uint32_t len, uint64_t n, uint32_t stride,
                   uint8_t *dst, void *stream);
 
+/* ---- batched packet generation: the pktgen loop (tests/lib.rs:756-788) ----
+ * The reference builds a packet with a `utils::create_*` builder (utils.rs:7-876), clones it,
+ * updates fields through the setters (headers.rs:340-344 -> set_bit_range 315-324) and serialises
+ * it with to_vec, once per packet.  Here the builder's bytes are a TEMPLATE: pkt_gen_create parses
+ * it once on the device (entry as for pkt_parse_batch) and places every generator field by its
+ * (header, occurrence, bits) in the template's chain (Index<&str> semantics, packet.rs:64-66);
+ * pkt_gen_run then writes n packets at dst + i*stride in one pass (the template, every field set
+ * to its value for that packet, the listed IPv4 checksums refreshed with Packet::ipv4_checksum
+ * (packet.rs:93-107) as the builders do, utils.rs:233-236; the rest of each stride slot zeroed).
+ * A field gets the value's low (end-start+1) <= 64 bits, as set_bit_range does.  Packet i of a
+ * run has global index g = first + i; the value of a field is
+ *   PKT_GEN_VALUES  values[f][i]                   (a DEVICE array per field, given to pkt_gen_run)
+ *   PKT_GEN_INC     base + step * (g % count)      (count 0: base + step * g; the reference's
+ *                                                   update loop is base 0, step 1, count 0xFFFF)
+ *   PKT_GEN_RANDOM  splitmix64(base + g)           (z = x + 0x9E3779B97F4A7C15;
+ *                   z = (z ^ z>>30) * 0xBF58476D1CE4E5B9; z = (z ^ z>>27) * 0x94D049BB133111EB;
+ *                   z ^ z>>31) — base is the seed.
+ * Fields apply in order (a later field wins where two overlap); checksum refreshes come last. */
+typedef enum pkt_gen_kind {
+    PKT_GEN_VALUES = 0,
+    PKT_GEN_INC    = 1,
+    PKT_GEN_RANDOM = 2
+} pkt_gen_kind_t;
+typedef struct pkt_gen_field {
+    pkt_field_spec_t field;  /* header type, occurrence, bits [start..=end], width 1..64 */
+    uint32_t kind;           /* pkt_gen_kind_t */
+    uint32_t reserved;
+    uint64_t base;
+    uint64_t step;
+    uint64_t count;
+} pkt_gen_field_t;
+typedef struct pkt_gen pkt_gen_t;
+size_t pkt_sizeof_gen_field(void);
+/* `tpl` is HOST memory (len bytes, <= 65535); at most 32 fields.  ipv4_csum_mask bit k refreshes
+ * the checksum of the template's k-th IPv4 header (at most 8).  Blocking (one template parse).
+ * Fails with PKT_ERR_INVALID_ARG if the template does not parse to PKT_OK or lacks a named header. */
+int pkt_gen_create(pkt_ctx_t *ctx, const uint8_t *tpl, uint32_t len, int entry,
+                   const pkt_gen_field_t *fields, uint32_t nfields, uint32_t ipv4_csum_mask,
+                   pkt_gen_t **gen);
+/* Writes packets first .. first+n-1 to `dst` (device, 16-byte aligned, n*stride bytes; stride a
+ * multiple of 16 and >= the template length).  `values` is a HOST array with one DEVICE pointer
+ * ([n] uint64) per field, used by PKT_GEN_VALUES fields (may be NULL when there are none).
+ * Asynchronous on `stream`. */
+int pkt_gen_run(pkt_gen_t *gen, uint64_t first, uint64_t n, uint32_t stride,
+                const uint64_t *const *values, uint8_t *dst, void *stream);
+int pkt_gen_destroy(pkt_gen_t *gen);
+
 /* Packet::ipv4_checksum (packet.rs:93-107) over n headers of 20 bytes at a fixed stride
  * in device memory: out[i] = checksum(hdrs + i*stride). */
 int pkt_ipv4_checksum_batch(pkt_ctx_t *ctx, const uint8_t *hdrs, uint32_t stride, uint64_t n,

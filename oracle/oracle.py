@@ -227,3 +227,18 @@ def ipv4_update_checksum(slab, n, chain, occurrence=0, stride=None, offsets=None
     L = lib()
     L.orc_ipv4_update_checksum.argtypes = [ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain), ctypes.c_uint32]
     L.orc_ipv4_update_checksum(ctypes.byref(b), ctypes.byref(ch), occurrence)
+
+
+def pktgen_loop(tpl, cnt, stride, mode="clone", first=0, nthreads=1, out=None, entry=0):
+    """tests/lib.rs:756-788 on the owned Packet model (clone / update+clone of a template; packet i
+    at out[i - first]).  The bench's CPU baseline for the generator."""
+    out = np.zeros((cnt, stride), np.uint8) if out is None else out
+    L = lib()
+    L.orc_pktgen_loop.restype = ctypes.c_int
+    L.orc_pktgen_loop.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    rc = L.orc_pktgen_loop(bytes(tpl), len(tpl), entry, {"clone": 0, "update": 1}[mode], first, cnt,
+                           out.ctypes.data, stride, nthreads)
+    if rc != 0:
+        raise RuntimeError(f"orc_pktgen_loop failed ({rc})")
+    return out

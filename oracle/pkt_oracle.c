@@ -803,3 +803,140 @@ int orc_ipv4_update_checksum(const pkt_batch_t *b, const pkt_chain_t *chain, uin
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------ pktgen loop (CPU baseline) */
+/* tests/lib.rs:756-788 pktgen_perf_test on the owned Packet model: Packet { hdrs: Vec<Box<dyn
+ * Header>>, payload: Vec<u8> } (lib.rs:129-134) with every header's bytes behind an
+ * Arc<Mutex<Vec<u8>>> (headers.rs:297-302).
+ *   clone   (mode 0): p = pkt.clone() (packet.rs:393-400: a Box per header, the Arc shared — Q13 —
+ *                     and the payload Vec copied), then p.to_vec() (packet.rs:385-392: one Vec
+ *                     grown header by header, each header's mutex locked to read it).
+ *   update  (mode 1): pkt["Ether"].set_etype(i % 0xFFFF) first — set_bit_range locks the header's
+ *                     mutex once per bit (headers.rs:315-324) — then the clone as above.
+ * Packet i's bytes go to out + i*stride (so the GPU generator's output can be compared with it).
+ * Each thread owns its own Packet (the reference loop is single-threaded). */
+typedef struct {
+    pthread_mutex_t mu;
+    int refs;
+    uint8_t *data;
+    size_t size;
+} orc_owned_hdr_t;
+
+typedef struct {
+    const uint8_t *tpl;
+    size_t len, payload_off;
+    const uint8_t *types;
+    const uint16_t *offs;
+    int nh, mode;
+    uint8_t *out;
+    size_t stride;
+    uint64_t lo, hi;
+} pg_job_t;
+
+static void *run_pg_job(void *arg) {
+    pg_job_t *j = (pg_job_t *)arg;
+    orc_owned_hdr_t *h = (orc_owned_hdr_t *)calloc((size_t)j->nh, sizeof(orc_owned_hdr_t));
+    int ether = -1;
+    for (int k = 0; k < j->nh; k++) {
+        pthread_mutex_init(&h[k].mu, NULL);
+        h[k].refs = 1;
+        h[k].size = (size_t)ORC_HDRS[j->types[k]].size;
+        h[k].data = (uint8_t *)malloc(h[k].size);
+        memcpy(h[k].data, j->tpl + j->offs[k], h[k].size);
+        if (ether < 0 && j->types[k] == PKT_HDR_ETHER) ether = k;
+    }
+    const size_t plen = j->len - j->payload_off;
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        if (j->mode == 1 && ether >= 0) {  /* set_etype: bits 96..111, one lock per bit */
+            uint64_t v = i % 0xFFFF;
+            for (size_t b = 112; b-- > 96;) {
+                pthread_mutex_lock(&h[ether].mu);
+                h[ether].data[b / 8] &= (uint8_t)~(1u << (7 - b % 8));
+                h[ether].data[b / 8] |= (uint8_t)((v & 1) << (7 - b % 8));
+                pthread_mutex_unlock(&h[ether].mu);
+                v >>= 1;
+            }
+        }
+        /* clone: a Box per header sharing the Arc, the payload copied */
+        orc_owned_hdr_t ***box = (orc_owned_hdr_t ***)malloc((size_t)j->nh * sizeof(*box));
+        for (int k = 0; k < j->nh; k++) {
+            box[k] = (orc_owned_hdr_t **)malloc(sizeof(**box));
+            *box[k] = &h[k];
+            __atomic_add_fetch(&h[k].refs, 1, __ATOMIC_RELAXED);
+        }
+        uint8_t *payload = (uint8_t *)malloc(plen ? plen : 1);
+        memcpy(payload, j->tpl + j->payload_off, plen);
+        /* to_vec: Vec::new() grown by extend_from_slice */
+        size_t cap = 0, n = 0;
+        uint8_t *vec = NULL;
+        for (int k = 0; k <= j->nh; k++) {
+            const uint8_t *src;
+            size_t sz;
+            orc_owned_hdr_t *hh = NULL;
+            if (k < j->nh) {
+                hh = *box[k];
+                pthread_mutex_lock(&hh->mu);
+                src = hh->data;
+                sz = hh->size;
+            } else {
+                src = payload;
+                sz = plen;
+            }
+            if (n + sz > cap) {
+                size_t nc = cap ? 2 * cap : 8;
+                while (nc < n + sz) nc *= 2;
+                vec = (uint8_t *)realloc(vec, nc);
+                cap = nc;
+            }
+            memcpy(vec + n, src, sz);
+            n += sz;
+            if (hh) pthread_mutex_unlock(&hh->mu);
+        }
+        memcpy(j->out + i * j->stride, vec, n);
+        free(vec);
+        free(payload);
+        for (int k = 0; k < j->nh; k++) {
+            __atomic_sub_fetch(&(*box[k])->refs, 1, __ATOMIC_RELAXED);
+            free(box[k]);
+        }
+        free(box);
+    }
+    for (int k = 0; k < j->nh; k++) {
+        pthread_mutex_destroy(&h[k].mu);
+        free(h[k].data);
+    }
+    free(h);
+    return NULL;
+}
+
+int orc_pktgen_loop(const uint8_t *tpl, size_t len, int entry, int mode, uint64_t first, uint64_t cnt,
+                    uint8_t *out, size_t stride, int nthreads) {
+    if (!tpl || !out || stride < len || mode < 0 || mode > 1 || entry < 0 || entry >= PKT_ENTRY_COUNT) return -1;
+    orc_pslice_t ps = {0};
+    walk_t w = {tpl, len, 0};
+    if (ENTRY_FNS[entry](&w, 0, &ps) != PKT_OK) { ps_free(&ps); return -1; }
+    uint8_t types[64];
+    uint16_t offs[64];
+    int nh = (int)(ps.n < 64 ? ps.n : 64);
+    for (int k = 0; k < nh; k++) {
+        types[k] = (uint8_t)ps.hdrs[k]->type;
+        offs[k] = (uint16_t)ps.hdrs[k]->off;
+    }
+    const size_t poff = ps.payload_off;
+    ps_free(&ps);
+    if (nthreads < 1) nthreads = 1;
+    pthread_t *th = (pthread_t *)calloc((size_t)nthreads, sizeof(pthread_t));
+    pg_job_t *jobs = (pg_job_t *)calloc((size_t)nthreads, sizeof(pg_job_t));
+    if (!th || !jobs) { free(th); free(jobs); return -1; }
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (pg_job_t){tpl, len, poff, types, offs, nh, mode, out - first * stride, stride,
+                             first + cnt * (uint64_t)t / (uint64_t)nthreads,
+                             first + cnt * (uint64_t)(t + 1) / (uint64_t)nthreads};
+        if (nthreads > 1) pthread_create(&th[t], NULL, run_pg_job, &jobs[t]);
+    }
+    if (nthreads == 1) run_pg_job(&jobs[0]);
+    else for (int t = 0; t < nthreads; t++) pthread_join(th[t], NULL);
+    free(th);
+    free(jobs);
+    return 0;
+}

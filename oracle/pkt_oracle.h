@@ -22,6 +22,8 @@ void orc_set_bit_range(uint8_t *map, size_t msb, size_t lsb, uint64_t value);
 int orc_set_fields(const pkt_batch_t *b, const pkt_chain_t *chain, const pkt_field_spec_t *specs,
                    uint32_t nspec, const uint64_t *const *values);
 int orc_ipv4_update_checksum(const pkt_batch_t *b, const pkt_chain_t *chain, uint32_t occurrence);
+int orc_pktgen_loop(const uint8_t *tpl, size_t len, int entry, int mode, uint64_t first, uint64_t cnt,
+                    uint8_t *out, size_t stride, int nthreads);
 long orc_slow_parse_to_vec(const uint8_t *p, size_t len, int entry, uint8_t *out, size_t cap);
 int orc_round_trip_batch(const pkt_batch_t *b, int entry, int slow, uint8_t *dst, uint64_t dst_len,
                          uint32_t *out_len, int nthreads);

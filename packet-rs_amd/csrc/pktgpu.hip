@@ -1,12 +1,12 @@
 // pktgpu.hip — kernels and the C ABI (include/pktgpu.h) of the MI355X batched parser.
 //
 // Kernels
-//   parse_kernel<NCH>     fast::parse_<entry> over a batch: LDS-DMA staging of NCH 16-byte
-//                         chunks per packet, the chain walk, and the fused field/checksum
-//                         extraction of the first Ether/Vlan/IPv4/IPv6/TCP/UDP (Q11).
-//   extract_kernel        batched make_header! getter for arbitrary (type, occurrence, bits).
-//   ipv4_csum_kernel      Packet::ipv4_checksum over a strided array of 20-byte headers.
-// (the device pcap indexer is in pktgpu_pcap.hip)
+//   parse_kernel<NCH>       fast::parse_<entry> over a batch: per-lane windows of NCH 16-byte
+//                           chunks staged in LDS, the chain walk, and the fused field/checksum
+//                           extraction of the first Ether/Vlan/IPv4/IPv6/TCP/UDP (Q11).
+//   parse_span_kernel<NCH>  the same with wave spans staged by LDS-DMA (pkt_ctx_set_staging 2).
+// (getters / to_vec / setters over a parsed batch: pktgpu_rewrite.hip; the device pcap indexer:
+// pktgpu_pcap.hip; packet generation: pktgpu_gen.hip)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -562,213 +562,6 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
 }
 
-// Batched `<Hdr>Slice::<field>()` (headers.rs:195-201 -> bit_range 252-263).
-struct XParams {
-    const uint8_t* slab;
-    uint64_t slab_len;
-    const uint64_t* offsets;
-    const uint32_t* lens;
-    uint32_t stride;
-    uint64_t n;
-    const uint8_t* n_hdrs;
-    const uint8_t* hdr_type;
-    const uint16_t* hdr_off;
-    pkt_field_spec_t spec;
-    uint64_t* values;
-    uint8_t* found;
-};
-
-__global__ __launch_bounds__(256) void extract_kernel(XParams p) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.n) return;
-    const uint32_t nh = p.n_hdrs[i];
-    int hit = -1;
-    uint32_t occ = 0;
-    for (uint32_t j = 0; j < nh && j < PKT_MAX_HDRS; j++) {
-        if (p.hdr_type[(uint64_t)j * p.n + i] == p.spec.hdr_type) {
-            if (occ == p.spec.occurrence) { hit = (int)j; break; }
-            occ++;
-        }
-    }
-    uint64_t v = 0;
-    if (hit >= 0) {
-        uint64_t off;
-        if (p.offsets) off = p.offsets[i];
-        else off = i * (uint64_t)p.stride;
-        const uint8_t* h = p.slab + off + p.hdr_off[(uint64_t)hit * p.n + i];
-        const uint32_t start = p.spec.start, end = p.spec.end;
-        const uint32_t w = end - start + 1;
-        // bits [s2..end] hold the low 64 bits of the field; bit_range's release-build shifts
-        // then keep the low (w mod 64, or 64) of them (headers.rs:262, Q8).
-        const uint32_t s2 = w > 64 ? end - 63 : start;
-        const uint32_t b0 = s2 >> 3, b1 = end >> 3;
-        uint64_t acc = 0, top = 0;  // top = the byte shifted out when 9 bytes are spanned
-        for (uint32_t b = b0; b <= b1; b++) {
-            top = acc >> 56;
-            acc = (acc << 8) | h[b];
-        }
-        const uint32_t r = 7 - (end & 7);
-        uint64_t val = r ? ((acc >> r) | (top << (64 - r))) : acc;
-        const uint32_t w2 = w > 64 ? (w & 63) : w;
-        if (w2 != 0 && w2 < 64) val &= (1ull << w2) - 1;
-        v = val;
-    }
-    p.values[i] = v;
-    if (p.found) p.found[i] = hit >= 0 ? 1 : 0;
-}
-
-// PacketSlice::to_vec (packet.rs:733-740): header slices in list order, then the payload.
-struct TParams {
-    const uint8_t* slab;
-    uint64_t slab_len;
-    const uint64_t* offsets;
-    const uint32_t* lens;
-    uint32_t stride;
-    uint64_t n;
-    const uint8_t* status;
-    const uint8_t* n_hdrs;
-    const uint8_t* hdr_type;
-    const uint16_t* hdr_off;
-    const uint16_t* payload_off;
-    const uint16_t* payload_len;
-    uint8_t* dst;
-    uint64_t dst_len;
-    const uint64_t* dst_offsets;
-    uint32_t* out_len;
-};
-
-__constant__ uint8_t kHdrSize[PKT_HDR_COUNT] = {0, 14, 4, 20, 40, 4, 20, 8, 28, 8, 14, 3, 5, 4, 4, 4, 4, 8, 12, 8, 35, 4};
-
-__global__ __launch_bounds__(256) void to_vec_kernel(TParams p) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.n) return;
-    uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
-    uint64_t doff = p.dst_offsets ? p.dst_offsets[i] : off;
-    if (p.status[i] != PKT_OK) {
-        if (p.out_len) p.out_len[i] = 0;
-        return;
-    }
-    const uint8_t* src = p.slab + off;
-    uint64_t cur = doff;
-    const uint32_t nh = p.n_hdrs[i];
-    for (uint32_t j = 0; j < nh && j < PKT_MAX_HDRS; j++) {
-        const uint32_t t = p.hdr_type[(uint64_t)j * p.n + i];
-        const uint32_t o = p.hdr_off[(uint64_t)j * p.n + i];
-        const uint32_t sz = t < PKT_HDR_COUNT ? kHdrSize[t] : 0;
-        for (uint32_t k = 0; k < sz; k++)
-            if (cur + k < p.dst_len) p.dst[cur + k] = src[o + k];
-        cur += sz;
-    }
-    const uint32_t po = p.payload_off[i], pl = p.payload_len[i];
-    for (uint32_t k = 0; k < pl; k++)
-        if (cur + k < p.dst_len) p.dst[cur + k] = src[po + k];
-    cur += pl;
-    if (p.out_len) p.out_len[i] = (uint32_t)(cur - doff);
-}
-
-// Batched set_bit_range (headers.rs:315-324) + in-place IPv4 checksum update.
-struct SParams {
-    uint8_t* slab;
-    uint64_t slab_len;
-    const uint64_t* offsets;
-    uint32_t stride;
-    uint64_t n;
-    const uint8_t* n_hdrs;
-    const uint8_t* hdr_type;
-    const uint16_t* hdr_off;
-};
-
-__device__ __forceinline__ int find_hdr(const SParams& p, uint64_t i, uint32_t type, uint32_t occurrence) {
-    const uint32_t nh = p.n_hdrs[i];
-    uint32_t occ = 0;
-    for (uint32_t j = 0; j < nh && j < PKT_MAX_HDRS; j++) {
-        if (p.hdr_type[(uint64_t)j * p.n + i] == type) {
-            if (occ == occurrence) return (int)j;
-            occ++;
-        }
-    }
-    return -1;
-}
-
-constexpr int kMaxSetSpecs = 16;
-struct SetSpecs {
-    pkt_field_spec_t spec[kMaxSetSpecs];
-    const uint64_t* values[kMaxSetSpecs];
-    uint32_t count;
-};
-
-__global__ __launch_bounds__(256) void set_fields_kernel(SParams p, SetSpecs ss) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.n) return;
-    const uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
-    for (uint32_t s = 0; s < ss.count; s++) {
-        const int j = find_hdr(p, i, ss.spec[s].hdr_type, ss.spec[s].occurrence);
-        if (j < 0) continue;
-        uint8_t* h = p.slab + off + p.hdr_off[(uint64_t)j * p.n + i];
-        const uint32_t lsb = ss.spec[s].start, msb = ss.spec[s].end;
-        uint64_t v = ss.values[s][i];
-        // set_bit_range: bit msb gets value bit 0, then upwards; value >>= 1 each step.  Done a
-        // byte at a time from the last byte of the field backwards.
-        int32_t b = (int32_t)msb;
-        while (b >= (int32_t)lsb) {
-            const uint32_t byte = (uint32_t)b >> 3;
-            const int32_t lo = max((int32_t)lsb, (int32_t)(byte * 8));  // first field bit in this byte
-            const uint32_t nb = (uint32_t)(b - lo + 1);                  // field bits in this byte
-            const uint32_t sh = 7 - ((uint32_t)b & 7);                   // bit b's position from the LSB
-            const uint32_t m = (((1u << nb) - 1u) << sh) & 0xFFu;
-            const uint32_t bits = ((uint32_t)(v & ((1ull << nb) - 1ull)) << sh) & 0xFFu;
-            h[byte] = (uint8_t)((h[byte] & ~m) | bits);
-            v = nb >= 64 ? 0 : (v >> nb);
-            b = lo - 1;
-        }
-    }
-}
-
-__global__ __launch_bounds__(256) void ipv4_update_kernel(SParams p, uint32_t occurrence) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= p.n) return;
-    const int j = find_hdr(p, i, PKT_HDR_IPV4, occurrence);
-    if (j < 0) return;
-    const uint64_t off = p.offsets ? p.offsets[i] : i * (uint64_t)p.stride;
-    uint8_t* h = p.slab + off + p.hdr_off[(uint64_t)j * p.n + i];
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 20; k += 2)
-        if (k != 10) s += ((uint32_t)h[k] << 8) | h[k + 1];
-    s = ((s >> 16) + s) & 0xFFFFu;
-    const uint32_t c = (~s) & 0xFFFFu;
-    h[10] = (uint8_t)(c >> 8);
-    h[11] = (uint8_t)c;
-}
-
-// n copies of one packet at a fixed stride, 16 bytes per lane per step (slot-contiguous).
-__global__ __launch_bounds__(256) void broadcast_kernel(const uint8_t* src, uint32_t len, uint64_t n,
-                                                        uint32_t stride, uint8_t* dst) {
-    const uint64_t total = n * (uint64_t)stride;  // bytes, multiple of 16 (checked by the host)
-    for (uint64_t q = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; q < total;
-         q += (uint64_t)gridDim.x * blockDim.x * 16) {
-        const uint32_t o = (uint32_t)(q % stride);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        u32x4 v;
-        uint8_t* b = reinterpret_cast<uint8_t*>(&v);
-#pragma unroll
-        for (int k = 0; k < 16; k++) b[k] = (o + k < len) ? src[o + k] : (uint8_t)0;
-        *reinterpret_cast<u32x4*>(dst + q) = v;
-    }
-}
-
-__global__ __launch_bounds__(256) void ipv4_csum_kernel(const uint8_t* hdrs, uint32_t stride, uint64_t n,
-                                                        uint16_t* out) {
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint8_t* v = hdrs + i * (uint64_t)stride;
-    uint32_t s = 0;
-#pragma unroll
-    for (int k = 0; k < 20; k += 2)
-        if (k != 10) s += ((uint32_t)v[k] << 8) | v[k + 1];
-    s = ((s >> 16) + s) & 0xFFFFu;
-    out[i] = (uint16_t)~s;
-}
 
 // How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
 enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
@@ -1169,174 +962,4 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     }
     return rc;
 }
-
-int pkt_extract_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
-                       const pkt_field_spec_t* specs, uint32_t nspec, uint64_t* const* values,
-                       uint8_t* const* found, void* stream) {
-    if (!ctx || !b || !chain || (nspec && (!specs || !values)))
-        return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (b->n == 0 || nspec == 0) return PKT_SUCCESS;
-    if (!chain->n_hdrs || !chain->hdr_type || !chain->hdr_off || !b->slab)
-        return fail(ctx, PKT_ERR_INVALID_ARG, "null chain column");
-    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
-    for (uint32_t s = 0; s < nspec; s++) {
-        const pkt_field_spec_t& sp = specs[s];
-        if (sp.hdr_type == 0 || sp.hdr_type >= PKT_HDR_COUNT || sp.end < sp.start ||
-            sp.end >= 8 * pkt_hdr_size(sp.hdr_type) || !values[s])
-            return fail(ctx, PKT_ERR_INVALID_ARG, "bad field spec");
-    }
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-    for (uint32_t s = 0; s < nspec; s++) {
-        XParams xp;
-        xp.slab = b->slab;
-        xp.slab_len = b->slab_len;
-        xp.offsets = b->offsets;
-        xp.lens = b->lens;
-        xp.stride = b->stride;
-        xp.n = b->n;
-        xp.n_hdrs = chain->n_hdrs;
-        xp.hdr_type = chain->hdr_type;
-        xp.hdr_off = chain->hdr_off;
-        xp.spec = specs[s];
-        xp.values = values[s];
-        xp.found = found ? found[s] : nullptr;
-        hipLaunchKernelGGL(extract_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, st, xp);
-        e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(ctx, e, "extract_kernel launch");
-    }
-    return PKT_SUCCESS;
-}
-
-int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* parsed, uint8_t* dst,
-                     uint64_t dst_len, const uint64_t* dst_offsets, uint32_t* out_len, void* stream) {
-    if (!ctx || !b || !parsed) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (b->n == 0) return PKT_SUCCESS;
-    if (!b->slab || !dst || !parsed->status || !parsed->n_hdrs || !parsed->hdr_type || !parsed->hdr_off ||
-        !parsed->payload_off || !parsed->payload_len)
-        return fail(ctx, PKT_ERR_INVALID_ARG, "null slab/dst/chain column");
-    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
-    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    TParams tp;
-    tp.slab = b->slab;
-    tp.slab_len = b->slab_len;
-    tp.offsets = b->offsets;
-    tp.lens = b->lens;
-    tp.stride = b->stride;
-    tp.n = b->n;
-    tp.status = parsed->status;
-    tp.n_hdrs = parsed->n_hdrs;
-    tp.hdr_type = parsed->hdr_type;
-    tp.hdr_off = parsed->hdr_off;
-    tp.payload_off = parsed->payload_off;
-    tp.payload_len = parsed->payload_len;
-    tp.dst = dst;
-    tp.dst_len = dst_len;
-    tp.dst_offsets = dst_offsets;
-    tp.out_len = out_len;
-    hipLaunchKernelGGL(to_vec_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), tp);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
-    return PKT_SUCCESS;
-}
-
-static int sparams(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain, SParams& sp) {
-    if (!b->slab || !chain || !chain->n_hdrs || !chain->hdr_type || !chain->hdr_off)
-        return fail(ctx, PKT_ERR_INVALID_ARG, "null slab/chain column");
-    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
-    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
-    sp.slab = const_cast<uint8_t*>(b->slab);
-    sp.slab_len = b->slab_len;
-    sp.offsets = b->offsets;
-    sp.stride = b->stride;
-    sp.n = b->n;
-    sp.n_hdrs = chain->n_hdrs;
-    sp.hdr_type = chain->hdr_type;
-    sp.hdr_off = chain->hdr_off;
-    return PKT_SUCCESS;
-}
-
-int pkt_set_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
-                   const pkt_field_spec_t* specs, uint32_t nspec, const uint64_t* const* values,
-                   void* stream) {
-    if (!ctx || !b || (nspec && (!specs || !values))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (b->n == 0 || nspec == 0) return PKT_SUCCESS;
-    SParams sp;
-    int rc = sparams(ctx, b, chain, sp);
-    if (rc) return rc;
-    for (uint32_t s = 0; s < nspec; s++) {
-        const pkt_field_spec_t& f = specs[s];
-        if (f.hdr_type == 0 || f.hdr_type >= PKT_HDR_COUNT || f.end < f.start ||
-            f.end >= 8 * pkt_hdr_size(f.hdr_type) || !values[s])
-            return fail(ctx, PKT_ERR_INVALID_ARG, "bad field spec");
-    }
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    // specs are applied in order inside one thread per packet (overlapping specs behave as
-    // sequential setter calls); batches of kMaxSetSpecs per launch, launches ordered on the stream
-    for (uint32_t s0 = 0; s0 < nspec; s0 += kMaxSetSpecs) {
-        SetSpecs ss;
-        ss.count = std::min<uint32_t>(kMaxSetSpecs, nspec - s0);
-        for (uint32_t k = 0; k < ss.count; k++) {
-            ss.spec[k] = specs[s0 + k];
-            ss.values[k] = values[s0 + k];
-        }
-        hipLaunchKernelGGL(set_fields_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
-                           reinterpret_cast<hipStream_t>(stream), sp, ss);
-        e = hipGetLastError();
-        if (e != hipSuccess) return hip_fail(ctx, e, "set_fields_kernel launch");
-    }
-    return PKT_SUCCESS;
-}
-
-int pkt_ipv4_update_checksum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
-                             uint32_t occurrence, void* stream) {
-    if (!ctx || !b) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (b->n == 0) return PKT_SUCCESS;
-    SParams sp;
-    int rc = sparams(ctx, b, chain, sp);
-    if (rc) return rc;
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    hipLaunchKernelGGL(ipv4_update_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), sp, occurrence);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "ipv4_update_kernel launch");
-    return PKT_SUCCESS;
-}
-
-int pkt_broadcast(pkt_ctx_t* ctx, const uint8_t* src, uint32_t len, uint64_t n, uint32_t stride,
-                  uint8_t* dst, void* stream) {
-    if (!ctx || (n && (!src || !dst))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (n == 0) return PKT_SUCCESS;
-    if (stride == 0 || stride % 16 || len > stride || ((uintptr_t)dst & 15))
-        return fail(ctx, PKT_ERR_INVALID_ARG, "stride must be a non-zero multiple of 16 >= len, dst 16-byte aligned");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    const uint64_t chunks = n * (uint64_t)stride / 16;
-    const unsigned grid = (unsigned)std::min<uint64_t>((chunks + 255) / 256, 256u * 64u);
-    hipLaunchKernelGGL(broadcast_kernel, dim3(grid), dim3(256), 0, reinterpret_cast<hipStream_t>(stream),
-                       src, len, n, stride, dst);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "broadcast_kernel launch");
-    return PKT_SUCCESS;
-}
-
-int pkt_ipv4_checksum_batch(pkt_ctx_t* ctx, const uint8_t* hdrs, uint32_t stride, uint64_t n,
-                            uint16_t* out, void* stream) {
-    if (!ctx || (n && (!hdrs || !out)) || (n && stride < 20)) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
-    if (n == 0) return PKT_SUCCESS;
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    hipLaunchKernelGGL(ipv4_csum_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
-                       reinterpret_cast<hipStream_t>(stream), hdrs, stride, n, out);
-    e = hipGetLastError();
-    if (e != hipSuccess) return hip_fail(ctx, e, "ipv4_csum_kernel launch");
-    return PKT_SUCCESS;
-}
-
 }  // extern "C"

@@ -503,4 +503,41 @@ __device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool 
     out = L.r;
 }
 
+// A 16-byte run of packet bytes as a 128-bit big-endian integer (bit 0 of the make_header!
+// numbering = the MSB of hi), for setting fields with one shift and mask (pktgpu_gen.hip,
+// pktgpu_rewrite.hip).
+struct U128 {
+    uint64_t hi, lo;  // big-endian: hi = bytes 0..7, lo = bytes 8..15
+};
+
+__device__ __forceinline__ U128 shl(U128 x, uint32_t s) {  // s < 128
+    if (s == 0) return x;
+    if (s >= 64) return {x.lo << (s - 64), 0};
+    return {(x.hi << s) | (x.lo >> (64 - s)), x.lo << s};
+}
+__device__ __forceinline__ U128 shr(U128 x, uint32_t s) {  // s < 128
+    if (s == 0) return x;
+    if (s >= 64) return {0, x.hi >> (s - 64)};
+    return {x.hi >> s, (x.lo >> s) | (x.hi << (64 - s))};
+}
+
+// set_bit_range (headers.rs:315-324) of bits [s, e] (MSB-first numbering, e - s < 64) to v's low w
+// bits, on the 128-bit run whose first bit is `b0` (the field overlaps the run; bits outside the
+// run are dropped).
+__device__ __forceinline__ void put_bits(U128& x, uint32_t s, uint32_t e, uint32_t w, uint64_t v, uint32_t b0) {
+    (void)s;
+    const uint64_t m = w >= 64 ? ~0ull : ((1ull << w) - 1ull);
+    const int32_t sh = 127 - ((int32_t)e - (int32_t)b0);  // where value bit 0 lands (from the LSB)
+    U128 V{0, v & m}, M{0, m};
+    if (sh >= 0) {
+        V = shl(V, (uint32_t)sh);
+        M = shl(M, (uint32_t)sh);
+    } else {
+        V = shr(V, (uint32_t)-sh);
+        M = shr(M, (uint32_t)-sh);
+    }
+    x.hi = (x.hi & ~M.hi) | V.hi;
+    x.lo = (x.lo & ~M.lo) | V.lo;
+}
+
 }  // namespace pktgpu

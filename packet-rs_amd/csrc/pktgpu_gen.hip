@@ -1,0 +1,390 @@
+// pktgpu_gen.hip — batched packet generation: the reference's pktgen loop
+// (tests/lib.rs:756-788: build a packet with a utils::create_* builder, clone it, update a field,
+// to_vec) as one device pass per batch.
+//
+// The builder runs once on the host and hands over its bytes (the template).  pkt_gen_create parses
+// the template ON THE DEVICE with the same walk as pkt_parse_batch (so a field named by (header,
+// occurrence, bits) resolves exactly as Packet's Index<&str> would find it, packet.rs:64-66) and
+// turns every field into an absolute MSB-first bit range of the packet.  pkt_gen_run then writes
+// n packets of `stride` bytes with one kernel.  Both kernels store the output as consecutive 1 KiB
+// per wave-instruction (a lane-per-packet kernel storing its 16-byte pieces at the packet stride
+// measured 5.5x slower on a 160-byte stride) and treat a 16-byte piece as a 128-bit big-endian
+// integer (bit 0 of the make_header! numbering = its MSB), where a field is set_bit_range
+// (headers.rs:315-324: the field's bits get the value's low `width` bits, bit `end` the value's
+// bit 0) by one shift and mask.
+//
+//   gen_region_kernel (fields or checksums, stride <= 1 KiB): one lane per packet; the wave's 64
+//   packets are built in LDS (template, then each field applied once per packet to the 1-2 pieces
+//   it overlaps, then Packet::ipv4_checksum (packet.rs:93-107, Q1 fold) of each refreshed IPv4
+//   header read back from the row, as the builders do, utils.rs:233-236), then stored.
+//   gen_kernel (pure clones, wider strides): one lane per 16-byte piece; a lane applies the fields
+//   overlapping its piece and, if it holds checksum bytes, rebuilds that IPv4 header's pieces.
+// Measured on test_tcp_packet (154 B, stride 160), 2^20 packets: clone 27 us (gen_kernel) / 30.5 us
+// (region); one INC field 30.9 us (region) vs 37 us (gen_kernel); 11 splitmix64 fields + checksum
+// 53.7 us (region) vs 351 us (gen_kernel: every field's value and shift computed for the whole wave).
+// Nothing is read back: HBM traffic = the slab written + the per-packet value arrays read
+// (PKT_GEN_VALUES fields only).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "pktgpu_ctx.hpp"
+#include "pktgpu_device.hpp"
+
+using pktgpu::U128;
+using pktgpu::put_bits;
+
+namespace {
+
+constexpr int kMaxGenFields = 32;
+constexpr int kMaxGenCsum = 8;
+constexpr uint32_t kGenBlock = 256;
+constexpr uint32_t kRegionMaxStride = 1024;  // gen_region_kernel: 64 * stride bytes of LDS per wave
+// pieces per launch: lane indices stay 32-bit (a launch covers whole packets)
+constexpr uint64_t kGenChunkPieces = 1ull << 31;
+
+struct GenField {
+    uint32_t s, e;        // absolute MSB-first bit range [s, e] in the packet (e - s < 64)
+    uint32_t kind;        // pkt_gen_kind_t
+    uint32_t w;           // e - s + 1
+    uint64_t base, step, count;
+    const uint64_t* values;  // PKT_GEN_VALUES: [n] of this launch
+};
+
+struct GenParams {
+    const uint8_t* tpl;   // device template, zero-padded to tpl_bytes (a multiple of 16)
+    uint8_t* dst;         // first packet of this launch
+    uint64_t first;       // global index of this launch's first packet (INC / RANDOM)
+    uint32_t tpl_bytes;
+    uint32_t ppp;         // 16-byte pieces per packet = stride / 16
+    uint32_t npieces;     // pieces of this launch (gen_kernel)
+    uint32_t npkts;       // packets of this launch (gen_region_kernel)
+    uint32_t nf, ncs;
+    uint32_t csum_at[kMaxGenCsum];  // byte offset of each refreshed IPv4 header
+    GenField f[kMaxGenFields];
+};
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Value of field f for packet i of this launch (global index g = first + i).
+__device__ __forceinline__ uint64_t field_value(const GenField& f, uint32_t i, uint64_t g) {
+    if (f.kind == PKT_GEN_VALUES) return f.values[i];
+    if (f.kind == PKT_GEN_RANDOM) return splitmix64(f.base + g);
+    uint64_t k = g;
+    if (f.count) k = (g < (1ull << 32) && f.count < (1ull << 32)) ? (uint64_t)((uint32_t)g % (uint32_t)f.count)
+                                                                    : g % f.count;
+    return f.base + f.step * k;
+}
+
+// Template piece k of packet i with every field applied (checksums not yet refreshed).
+__device__ __forceinline__ U128 build_piece(const GenParams& p, uint32_t k, uint32_t i, uint64_t g) {
+    U128 x{0, 0};
+    const uint32_t b = k * 16u;
+    if (b < p.tpl_bytes) {
+        const uint4 t = *reinterpret_cast<const uint4*>(p.tpl + b);
+        x.hi = ((uint64_t)__builtin_bswap32(t.x) << 32) | __builtin_bswap32(t.y);
+        x.lo = ((uint64_t)__builtin_bswap32(t.z) << 32) | __builtin_bswap32(t.w);
+    }
+    const uint32_t b0 = b * 8u;
+    for (uint32_t j = 0; j < p.nf; j++) {  // uniform loop
+        const GenField& f = p.f[j];
+        if (f.s <= b0 + 127u && f.e >= b0) put_bits(x, f.s, f.e, f.w, field_value(f, i, g), b0);
+    }
+    return x;
+}
+
+// byte q (0..47) of three consecutive pieces (selects, not an indexed array: no scratch)
+__device__ __forceinline__ uint32_t byte3(const U128& w0, const U128& w1, const U128& w2, uint32_t q) {
+    const uint32_t sel = q >> 4;
+    const U128 x = sel == 0 ? w0 : (sel == 1 ? w1 : w2);
+    const uint32_t r = q & 15u;
+    const uint64_t h = r < 8 ? x.hi : x.lo;
+    return (uint32_t)(h >> (8u * (7u - (r & 7u)))) & 0xFFu;
+}
+
+// Packet::ipv4_checksum's folded sum (packet.rs:93-107, Q1) over the IPv4 header at byte hb of
+// packet i as generated; piece `have` (== x) is reused, the others are rebuilt.
+__device__ __forceinline__ uint32_t ipv4_sum(const GenParams& p, uint32_t hb, uint32_t have, const U128& x,
+                                             uint32_t i, uint64_t g) {
+    const uint32_t k0 = hb >> 4, r = hb & 15u;
+    const U128 w0 = k0 == have ? x : build_piece(p, k0, i, g);
+    const U128 w1 = k0 + 1u == have ? x : build_piece(p, k0 + 1u, i, g);
+    const U128 w2 = r + 20u > 32u ? (k0 + 2u == have ? x : build_piece(p, k0 + 2u, i, g)) : U128{0, 0};
+    uint32_t s = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 20; j += 2)
+        if (j != 10) s += (byte3(w0, w1, w2, r + j) << 8) | byte3(w0, w1, w2, r + j + 1);
+    return ((s >> 16) + s) & 0xFFFFu;  // packet.rs:102-104 (Q1)
+}
+
+__device__ __forceinline__ void store_piece(uint8_t* at, const U128& x) {
+    uint4 o;
+    o.x = __builtin_bswap32((uint32_t)(x.hi >> 32));
+    o.y = __builtin_bswap32((uint32_t)x.hi);
+    o.z = __builtin_bswap32((uint32_t)(x.lo >> 32));
+    o.w = __builtin_bswap32((uint32_t)x.lo);
+    *reinterpret_cast<uint4*>(at) = o;
+}
+
+__global__ __launch_bounds__(kGenBlock) void gen_kernel(GenParams p) {
+    const uint32_t q = blockIdx.x * kGenBlock + threadIdx.x;
+    if (q >= p.npieces) return;
+    const uint32_t i = q / p.ppp;       // packet within this launch
+    const uint32_t k = q - i * p.ppp;   // piece within the packet
+    const uint64_t g = p.first + i;
+    U128 x = build_piece(p, k, i, g);
+    // IPv4 checksum refresh: the lane holding bytes hb+10 / hb+11 rebuilds the header's pieces
+    for (uint32_t c = 0; c < p.ncs; c++) {
+        const uint32_t hb = p.csum_at[c];
+        const uint32_t cb = hb + 10u;
+        if (cb + 1u < k * 16u || cb >= k * 16u + 16u) continue;
+        const uint32_t s = ipv4_sum(p, hb, k, x, i, g);
+        put_bits(x, cb * 8u, cb * 8u + 15u, 16u, (uint64_t)(~s & 0xFFFFu), k * 128u);
+    }
+    store_piece(p.dst + (uint64_t)q * 16u, x);
+}
+
+// One lane per packet, the wave's WHOLE output region (64 packets x stride) built in LDS (one
+// wave per block), then stored with the contiguous 1 KiB-per-instruction shape of gen_kernel.  Each
+// lane writes the template into its row, then applies the fields in order — one field at a time,
+// read-modify-write of the 1-2 pieces it overlaps, so a field's parameters are read once per
+// packet group and its value computed once per packet — then refreshes the checksums from the row.
+__device__ __forceinline__ U128 lds_get(const uint8_t* at) {
+    const uint4 t = *reinterpret_cast<const uint4*>(at);
+    return U128{((uint64_t)__builtin_bswap32(t.x) << 32) | __builtin_bswap32(t.y),
+                ((uint64_t)__builtin_bswap32(t.z) << 32) | __builtin_bswap32(t.w)};
+}
+__device__ __forceinline__ void lds_put(uint8_t* at, const U128& x) {
+    *reinterpret_cast<uint4*>(at) = make_uint4(__builtin_bswap32((uint32_t)(x.hi >> 32)), __builtin_bswap32((uint32_t)x.hi),
+                                               __builtin_bswap32((uint32_t)(x.lo >> 32)), __builtin_bswap32((uint32_t)x.lo));
+}
+
+__global__ __launch_bounds__(64) void gen_region_kernel(GenParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t region[];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t w0 = blockIdx.x * 64u;
+    const uint32_t i = w0 + lane;
+    const bool act = i < p.npkts;
+    const uint64_t g = p.first + i;
+    const uint32_t stride = p.ppp * 16u;
+    uint8_t* row = region + lane * stride;
+    for (uint32_t k = 0; k < p.ppp; k++) {  // the template (zeros past it)
+        uint4 t = make_uint4(0, 0, 0, 0);
+        if (k * 16u < p.tpl_bytes) t = *reinterpret_cast<const uint4*>(p.tpl + k * 16u);
+        *reinterpret_cast<uint4*>(row + k * 16u) = t;
+    }
+    for (uint32_t j = 0; j < p.nf; j++) {  // fields in order (uniform)
+        const GenField& f = p.f[j];
+        const uint64_t v = act ? field_value(f, i, g) : 0;
+        for (uint32_t k = f.s >> 7; k <= (f.e >> 7); k++) {
+            U128 x = lds_get(row + k * 16u);
+            put_bits(x, f.s, f.e, f.w, v, k * 128u);
+            lds_put(row + k * 16u, x);
+        }
+    }
+    for (uint32_t c = 0; c < p.ncs; c++) {  // checksums last (uniform)
+        const uint32_t hb = p.csum_at[c], k0 = hb >> 4, r = hb & 15u;
+        const U128 x0 = lds_get(row + k0 * 16u), x1 = lds_get(row + k0 * 16u + 16u);
+        const U128 x2 = r + 20u > 32u ? lds_get(row + k0 * 16u + 32u) : U128{0, 0};
+        uint32_t sum = 0;
+#pragma unroll
+        for (uint32_t j = 0; j < 20; j += 2)
+            if (j != 10) sum += (byte3(x0, x1, x2, r + j) << 8) | byte3(x0, x1, x2, r + j + 1);
+        const uint32_t cv = ~(((sum >> 16) + sum) & 0xFFFFu) & 0xFFFFu;  // packet.rs:102-104 (Q1)
+        const uint32_t cb = hb + 10u;
+        for (uint32_t k = cb >> 4; k <= ((cb + 1u) >> 4); k++) {
+            U128 x = lds_get(row + k * 16u);
+            put_bits(x, cb * 8u, cb * 8u + 15u, 16u, cv, k * 128u);
+            lds_put(row + k * 16u, x);
+        }
+    }
+    __syncthreads();
+    const uint32_t npk = p.npkts - w0 < 64u ? p.npkts - w0 : 64u;
+    const uint32_t bytes = npk * stride;
+    uint8_t* d = p.dst + (uint64_t)w0 * stride;
+    for (uint32_t o = lane * 16u; o < bytes; o += 1024u)
+        *reinterpret_cast<uint4*>(d + o) = *reinterpret_cast<const uint4*>(region + o);
+}
+
+}  // namespace
+
+struct pkt_gen {
+    pkt_ctx_t* ctx = nullptr;
+    uint8_t* tpl = nullptr;  // device, zero-padded to tpl_bytes
+    uint32_t len = 0, tpl_bytes = 0;
+    std::vector<GenField> fields;
+    std::vector<uint32_t> csum_at;
+};
+
+extern "C" {
+
+size_t pkt_sizeof_gen_field(void) { return sizeof(pkt_gen_field_t); }
+
+int pkt_gen_create(pkt_ctx_t* ctx, const uint8_t* tpl, uint32_t len, int entry, const pkt_gen_field_t* fields,
+                   uint32_t nfields, uint32_t ipv4_csum_mask, pkt_gen_t** out) {
+    if (!ctx || !out || !tpl || len == 0 || (nfields && !fields)) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    *out = nullptr;
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    if (len > 0xFFFFu) return fail(ctx, PKT_ERR_INVALID_ARG, "template longer than 65535 bytes");
+    if (nfields > (uint32_t)kMaxGenFields) return fail(ctx, PKT_ERR_INVALID_ARG, "more than 32 fields");
+    for (uint32_t j = 0; j < nfields; j++) {
+        const pkt_field_spec_t& f = fields[j].field;
+        if (f.hdr_type == 0 || f.hdr_type >= PKT_HDR_COUNT || f.end < f.start || f.end - f.start >= 64 ||
+            f.end >= 8 * pkt_hdr_size(f.hdr_type) || fields[j].kind > PKT_GEN_RANDOM)
+            return fail(ctx, PKT_ERR_INVALID_ARG, "bad generator field (width 1..64 bits inside its header)");
+    }
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+
+    // Parse the template on the device (chain columns of one packet) to place every field.
+    const uint32_t tb = (len + 15u) & ~15u;
+    uint8_t* dtpl = nullptr;
+    uint8_t* dcol = nullptr;  // status, n_hdrs, hdr_type[16], hdr_off[16], lens[1]
+    if ((e = hipMalloc(reinterpret_cast<void**>(&dtpl), tb)) != hipSuccess ||
+        (e = hipMalloc(reinterpret_cast<void**>(&dcol), 256)) != hipSuccess) {
+        (void)hipFree(dtpl);
+        return hip_fail(ctx, e, "hipMalloc (generator template)");
+    }
+    std::vector<uint8_t> padded(tb, 0);
+    std::memcpy(padded.data(), tpl, len);
+    pkt_out_t o;
+    std::memset(&o, 0, sizeof(o));
+    o.status = dcol;
+    o.n_hdrs = dcol + 16;
+    o.hdr_type = dcol + 32;
+    o.hdr_off = reinterpret_cast<uint16_t*>(dcol + 64);
+    uint32_t* dlen = reinterpret_cast<uint32_t*>(dcol + 128);
+    pkt_batch_t b;
+    std::memset(&b, 0, sizeof(b));
+    b.slab = dtpl;
+    b.slab_len = tb;  // >= 16; the packet itself is `len` bytes (lens)
+    b.lens = dlen;
+    b.stride = tb;
+    b.n = 1;
+    uint8_t st = 0, nh = 0, ty[PKT_MAX_HDRS] = {};
+    uint16_t off[PKT_MAX_HDRS] = {};
+    int rc = PKT_SUCCESS;
+    e = hipMemcpy(dtpl, padded.data(), tb, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(dlen, &len, 4, hipMemcpyHostToDevice);
+    if (e == hipSuccess) {
+        rc = pkt_parse_batch(ctx, &b, entry, &o, nullptr);
+        if (rc == PKT_SUCCESS) {
+            e = hipDeviceSynchronize();
+            if (e == hipSuccess) e = hipMemcpy(&st, o.status, 1, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(&nh, o.n_hdrs, 1, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(ty, o.hdr_type, PKT_MAX_HDRS, hipMemcpyDeviceToHost);
+            if (e == hipSuccess) e = hipMemcpy(off, o.hdr_off, 2 * PKT_MAX_HDRS, hipMemcpyDeviceToHost);
+        }
+    }
+    (void)hipFree(dcol);
+    if (rc == PKT_SUCCESS && e != hipSuccess) rc = hip_fail(ctx, e, "template parse");
+    if (rc == PKT_SUCCESS && st != PKT_OK) rc = fail(ctx, PKT_ERR_INVALID_ARG, "template does not parse (status not OK)");
+    auto find = [&](uint32_t type, uint32_t occ) -> int {
+        for (uint32_t j = 0, c = 0; j < nh; j++)
+            if (ty[j] == type && c++ == occ) return (int)off[j];
+        return -1;
+    };
+    pkt_gen* G = nullptr;
+    if (rc == PKT_SUCCESS) {
+        G = new pkt_gen();
+        G->ctx = ctx;
+        G->len = len;
+        G->tpl_bytes = tb;
+        for (uint32_t j = 0; j < nfields && rc == PKT_SUCCESS; j++) {
+            const pkt_gen_field_t& f = fields[j];
+            const int at = find(f.field.hdr_type, f.field.occurrence);
+            if (at < 0) { rc = fail(ctx, PKT_ERR_INVALID_ARG, "generator field: header not in the template's chain"); break; }
+            GenField gf;
+            gf.s = (uint32_t)at * 8u + f.field.start;
+            gf.e = (uint32_t)at * 8u + f.field.end;
+            gf.w = gf.e - gf.s + 1u;
+            gf.kind = f.kind;
+            gf.base = f.base;
+            gf.step = f.step;
+            gf.count = f.count;
+            gf.values = nullptr;
+            G->fields.push_back(gf);
+        }
+        for (uint32_t occ = 0; occ < 32 && rc == PKT_SUCCESS; occ++) {
+            if (!(ipv4_csum_mask >> occ & 1u)) continue;
+            const int at = find(PKT_HDR_IPV4, occ);
+            if (at < 0) { rc = fail(ctx, PKT_ERR_INVALID_ARG, "checksum mask names an IPv4 header the template lacks"); break; }
+            if (G->csum_at.size() == (size_t)kMaxGenCsum) { rc = fail(ctx, PKT_ERR_INVALID_ARG, "more than 8 checksum refreshes"); break; }
+            G->csum_at.push_back((uint32_t)at);
+        }
+    }
+    if (rc != PKT_SUCCESS) {
+        delete G;
+        (void)hipFree(dtpl);
+        return rc;
+    }
+    G->tpl = dtpl;
+    *out = G;
+    return PKT_SUCCESS;
+}
+
+int pkt_gen_destroy(pkt_gen_t* g) {
+    if (!g) return PKT_SUCCESS;
+    if (g->tpl) {
+        (void)hipSetDevice(g->ctx->device);
+        (void)hipDeviceSynchronize();  // runs still in flight read the template
+        (void)hipFree(g->tpl);
+    }
+    delete g;
+    return PKT_SUCCESS;
+}
+
+int pkt_gen_run(pkt_gen_t* g, uint64_t first, uint64_t n, uint32_t stride, const uint64_t* const* values,
+                uint8_t* dst, void* stream) {
+    if (!g) return PKT_ERR_INVALID_ARG;
+    pkt_ctx_t* ctx = g->ctx;
+    if (n == 0) return PKT_SUCCESS;
+    if (!dst || ((uintptr_t)dst & 15)) return fail(ctx, PKT_ERR_INVALID_ARG, "dst null or not 16-byte aligned");
+    if (stride == 0 || stride % 16 || stride < g->len)
+        return fail(ctx, PKT_ERR_INVALID_ARG, "stride must be a multiple of 16 and >= the template length");
+    for (size_t j = 0; j < g->fields.size(); j++)
+        if (g->fields[j].kind == PKT_GEN_VALUES && (!values || !values[j]))
+            return fail(ctx, PKT_ERR_INVALID_ARG, "PKT_GEN_VALUES field without a value array");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    GenParams p;
+    std::memset(&p, 0, sizeof(p));
+    p.tpl = g->tpl;
+    p.tpl_bytes = std::min<uint32_t>(g->tpl_bytes, stride);
+    p.ppp = stride / 16;
+    p.nf = (uint32_t)g->fields.size();
+    p.ncs = (uint32_t)g->csum_at.size();
+    for (uint32_t c = 0; c < p.ncs; c++) p.csum_at[c] = g->csum_at[c];
+    const uint64_t per = std::max<uint64_t>(1, kGenChunkPieces / p.ppp);  // packets per launch
+    for (uint64_t i0 = 0; i0 < n; i0 += per) {
+        const uint64_t m = std::min(per, n - i0);
+        for (uint32_t j = 0; j < p.nf; j++) {
+            p.f[j] = g->fields[j];
+            if (p.f[j].kind == PKT_GEN_VALUES) p.f[j].values = values[j] + i0;
+        }
+        p.first = first + i0;
+        p.dst = dst + i0 * stride;
+        p.npieces = (uint32_t)(m * p.ppp);
+        p.npkts = (uint32_t)m;
+        // region kernel whenever a field or checksum is applied and the 64-packet region fits LDS;
+        // pure clones (and strides over 1 KiB) take the lane-per-piece kernel
+        if ((p.nf || p.ncs) && stride <= kRegionMaxStride)
+            hipLaunchKernelGGL(gen_region_kernel, dim3((p.npkts + 63) / 64), dim3(64), 64 * stride,
+                               reinterpret_cast<hipStream_t>(stream), p);
+        else
+            hipLaunchKernelGGL(gen_kernel, dim3((p.npieces + kGenBlock - 1) / kGenBlock), dim3(kGenBlock), 0,
+                               reinterpret_cast<hipStream_t>(stream), p);
+        e = hipGetLastError();
+        if (e != hipSuccess) return hip_fail(ctx, e, "gen_kernel launch");
+    }
+    return PKT_SUCCESS;
+}
+
+}  // extern "C"

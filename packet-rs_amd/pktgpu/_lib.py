@@ -37,6 +37,11 @@ class PktFieldSpec(ctypes.Structure):
                 ("reserved", ctypes.c_uint16)]
 
 
+class PktGenField(ctypes.Structure):
+    _fields_ = [("field", PktFieldSpec), ("kind", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
+                ("base", ctypes.c_uint64), ("step", ctypes.c_uint64), ("count", ctypes.c_uint64)]
+
+
 # Every function declared in include/pktgpu.h: name -> (restype, argtypes)
 _P = ctypes.c_void_p
 SIGNATURES = {
@@ -76,6 +81,13 @@ SIGNATURES = {
     "pkt_ipv4_update_checksum": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
                                                 ctypes.c_uint32, _P]),
     "pkt_broadcast": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, _P, _P]),
+    "pkt_sizeof_gen_field": (ctypes.c_size_t, []),
+    "pkt_gen_create": (ctypes.c_int, [_P, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_int,
+                                      ctypes.POINTER(PktGenField), ctypes.c_uint32, ctypes.c_uint32,
+                                      ctypes.POINTER(_P)]),
+    "pkt_gen_run": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                   ctypes.POINTER(_P), _P, _P]),
+    "pkt_gen_destroy": (ctypes.c_int, [_P]),
     "pkt_ipv4_checksum_batch": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, _P, _P]),
     "pkt_pcap_index": (ctypes.c_int, [_P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
                                       ctypes.POINTER(ctypes.c_uint64)]),
@@ -123,7 +135,8 @@ def load():
     if L.pkt_abi_version() != schema.ABI_VERSION:
         raise ImportError("libpktgpu ABI version mismatch")
     if L.pkt_sizeof_out() != ctypes.sizeof(PktOut) or L.pkt_sizeof_batch() != ctypes.sizeof(PktBatch) \
-            or L.pkt_sizeof_field_spec() != ctypes.sizeof(PktFieldSpec):
+            or L.pkt_sizeof_field_spec() != ctypes.sizeof(PktFieldSpec) \
+            or L.pkt_sizeof_gen_field() != ctypes.sizeof(PktGenField):
         raise ImportError("libpktgpu struct layout mismatch with pktgpu/_lib.py")
     _lib = L
     return L

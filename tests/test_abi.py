@@ -33,7 +33,7 @@ def test_library_builds_and_loads(L):
 
 def test_every_declared_symbol_is_exported(L):
     names = declared_functions()
-    assert len(names) == 44
+    assert len(names) == 48
     for n in names:
         assert hasattr(L, n), n
     assert set(names) == set(_lib.SIGNATURES), "pktgpu/_lib.py SIGNATURES out of sync with pktgpu.h"
@@ -43,6 +43,7 @@ def test_struct_layouts(L):
     assert L.pkt_sizeof_out() == ctypes.sizeof(_lib.PktOut) == 8 * len(schema.COLUMN_NAMES)
     assert L.pkt_sizeof_batch() == ctypes.sizeof(_lib.PktBatch)
     assert L.pkt_sizeof_field_spec() == ctypes.sizeof(_lib.PktFieldSpec) == 8
+    assert L.pkt_sizeof_gen_field() == ctypes.sizeof(_lib.PktGenField) == 40
 
 
 def test_metadata_tables_match_oracle(L):

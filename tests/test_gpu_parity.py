@@ -368,6 +368,38 @@ def test_to_vec_templates_and_gre_reorder_vs_oracle(P):
     assert reordered == 4  # the four GRE packets, each with >= 2 options (Q2)
 
 
+@pytest.mark.parametrize("shift", [0, 1, 6])
+def test_to_vec_c4_dst_layouts_vs_oracle(P, shift):
+    """C4 records (plus Q2 GRE packets and truncated ones) serialised into a packed destination
+    whose records start `shift` bytes off the source's 16-byte phase: the kernel's aligned
+    16-byte path (shift 0 keeps the phase), its dword path and the Q2 gather all equal the
+    oracle's slow::parse(..).to_vec() (tests/lib.rs:790-802)."""
+    n = 1 << 16
+    slab, offs, lens = gen.gen_c4(n, seed=11)
+    rng = np.random.default_rng(shift)
+    cut = rng.random(n) < 0.02  # some truncated records: nothing written, out_len 0
+    lens = np.where(cut, (lens * rng.random(n)).astype(np.uint32), lens).astype(np.uint32)
+    ds, do, dl = dev(slab), dev(offs), dev(lens)
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst_off = (offs + np.uint64(shift)) if shift == 0 else \
+        (np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + np.uint64(3))[:-1]]) + np.uint64(shift))
+    dst_len = int(dst_off[-1]) + int(lens[-1]) + 64
+    dst = torch.full((dst_len,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst, dst_offsets=dev(dst_off.astype(np.uint64)))
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    want, wl = oracle.round_trip_batch(slab, n, offsets=offs, lens=lens, slow=True, nthreads=8)
+    assert np.array_equal(ln, wl)
+    for i in range(n):
+        a, b, k = int(offs[i]), int(dst_off[i]), int(wl[i])
+        assert o[b:b + k].tobytes() == want[a:a + k].tobytes(), i
+    # nothing outside the written records changed
+    mask = np.ones(dst_len, bool)
+    for i in range(n):
+        mask[int(dst_off[i]):int(dst_off[i]) + int(wl[i])] = False
+    assert (o[mask] == 0xEE).all()
+
+
 # ------------------------------------------------------------------ in-block steering (sort)
 @pytest.mark.parametrize("mode", [1, 2])
 def test_sort_modes_bit_exact(P, mode):
