@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PKTGPU_ABI_VERSION 2
+#define PKTGPU_ABI_VERSION 3
 
 /* Maximum number of headers recorded per packet.  The reference recursion is unbounded
  * (fast.rs:53 VLAN stacks, :69 MPLS stacks, :89/:92/:104/:107 IP-in-IP, :168/:186/:219
@@ -249,11 +249,6 @@ const char *pkt_ctx_last_error(const pkt_ctx_t *ctx);
 /* Tuning knob: packets staged per wave window (bytes of each packet copied to LDS).
  * 0 = automatic.  Values are rounded to a multiple of 16 and clamped to [16, 256]. */
 int         pkt_ctx_set_window(pkt_ctx_t *ctx, uint32_t window_bytes);
-/* Tuning knob: before walking, sort each block of 256 packets by a chain-class key (EtherType
- * after VLAN tags, IP protocol) so each wave walks packets of one layout; outputs still land at
- * the packets' own indices.  0 = auto (currently: off — the barriers and result staging cost
- * more than the uniform waves save on the measured mixes), 1 = always, 2 = never. */
-int         pkt_ctx_set_sort(pkt_ctx_t *ctx, int mode);
 /* Fast path (default on).  For entries PARSE and ETHERNET, a packet that starts on a 16-byte
  * boundary and whose first bytes read Ether / 0-2 x Vlan / IPv4 / UDP (dst != 4789) or TCP, long
  * enough for every header, has its chain decided by a few compares on the registers its bytes
@@ -264,7 +259,7 @@ int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
 /* Tuning knob: how packet bytes reach LDS.  0 = automatic (currently 1), 1 = per-lane windows of
  * pkt_ctx_set_window bytes (deeper headers read through L2), 2 = wave spans: each wave of 64
  * packets copies the contiguous byte range its packets occupy (up to 16 KiB; else per-lane
- * windows) into LDS by LDS-DMA and walks every header from there.  Not with the sorted path.
+ * windows) into LDS by LDS-DMA and walks every header from there.
  * Results are identical in every mode. */
 int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 

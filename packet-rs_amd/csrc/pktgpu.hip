@@ -168,40 +168,8 @@ __device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint6
     if (len > 0xFFFFu) len = 0xFFFFu;  // u16 offsets/lengths in the ABI
 }
 
-// Chain-class key of a staged packet (6 bits): the EtherType after up to two VLAN tags and the
-// IP protocol behind it.  Packets with one key walk (nearly) the same states, so sorting a block
-// by key makes its waves walk one case per header instead of one per distinct state.
-__device__ __forceinline__ uint32_t class_key(const PacketView& pv, bool active) {
-    if (!active || pv.len < 14) return 63u;
-    uint32_t et = pv.be16(12), o = 14, v = 0;
-    if (et == 0x8100u && pv.len >= o + 4) { et = pv.be16(o + 2); o += 4; v = 1; }
-    if (et == 0x8100u && pv.len >= o + 4) { et = pv.be16(o + 2); o += 4; v = 2; }
-    uint32_t pr = 0;
-    if (et == 0x0800u && pv.len >= o + 10) pr = pv.u8(o + 9);
-    else if (et == 0x86DDu && pv.len >= o + 7) pr = pv.u8(o + 6);
-    const uint32_t cls = et < 1500u ? 0u : et == 0x0800u ? 1u : et == 0x86DDu ? 2u : et == 0x0806u ? 3u : 4u;
-    // protocol class: TCP, UDP, or "other next header" (GRE, ICMP, IP-in-IP); 0 = payload
-    const uint32_t pc = pr == 6u ? 1u : pr == 17u ? 2u
-                      : (pr == 47u || pr == 1u || pr == 58u || pr == 4u || pr == 41u) ? 3u : 0u;
-    return (cls * 3u + v) * 4u + pc;  // <= 59 for an active packet; 63 = inactive
-}
-
-// Dynamic-LDS carve of a parse block (base 16-byte aligned; nothing static in front of it).
-//   [0, window_lds(NCH))     packet windows, packet-major (packet q at q * lane_stride(NCH))
-//   sort part (p.sort only): bucket counts, permutation, the walk results of the 256 packets
-struct SortLds {
-    uint32_t hist[64];
-    uint32_t key0, mixed, pad[2];
-    uint16_t perm[kBlock];
-    uint8_t slot_type[PKT_MAX_HDRS][kBlock];
-    uint16_t slot_off[PKT_MAX_HDRS][kBlock];
-    uint8_t status[kBlock], n[kBlock];
-    uint16_t poff[kBlock];
-    uint32_t mask[kBlock];
-    int16_t first[6][kBlock];
-};
-
-// packet-major: packet q's window at q * lane_stride, lane_stride = 4*NCH+1 dwords (odd, so the
+// Dynamic LDS of a parse block (base 16-byte aligned; nothing static in front of it): the packet
+// windows, packet-major: packet q's window at q * lane_stride, lane_stride = 4*NCH+1 dwords (odd, so the
 // per-lane dword reads of the walk hit 64 distinct banks); +16 B for the last lane's over-read.
 // (A chunk-major layout with ds_write_b128 staging had 4-way conflicts on the walk's reads: C4
 // 3 % slower, C2/C3 neutral, scripts/ab_bench.sh.)
@@ -209,6 +177,8 @@ __host__ __device__ constexpr uint32_t lane_stride(int nch) { return (uint32_t)(
 __host__ __device__ constexpr size_t window_lds(int nch) {
     return ((size_t)kBlock * lane_stride(nch) + 16 + 15) & ~(size_t)15;
 }
+// the lockstep walk's first-offset slots: u16 [type 0..7][lane], after the windows / the span region
+constexpr size_t first_lds(uint32_t lanes) { return 8u * lanes * sizeof(uint16_t); }
 
 __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
                                                 uint32_t len, int nch) {
@@ -218,6 +188,7 @@ __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, 
     pv.off = off;
     pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
     pv.shift = (uint32_t)(off & 15);
+    pv.win_lo = 0;
     pv.win_end = (uint32_t)nch * 16u - pv.shift;
     pv.len = len;
     return pv;
@@ -272,8 +243,8 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
-template <int NCH, uint32_t GM, int WK>
-__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortLds& S, uint32_t base,
+template <int NCH, uint32_t GM, int WK, bool STAGED = false>
+__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own);
 
@@ -287,24 +258,67 @@ template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
 void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    SortLds& S = *reinterpret_cast<SortLds*>(lds + window_lds(NCH));  // only touched if p.sort
     const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
     const bool act = base + threadIdx.x < p.n;
     u32x4 chunk[NCH];
     uint64_t off;
     uint32_t len;
+    if constexpr (WK == 1 && NCH >= 4) {
+        // Indexed batches: the wave loads its 64 windows cooperatively — in load k, lanes 4j..4j+3
+        // fetch chunks 0-3 of packet 16k + j, i.e. 64 contiguous bytes per 4 lanes instead of one
+        // scattered 16-byte piece per lane (the per-lane shape is request-bound: 42 us for the
+        // 2^20 C4 windows alone, scripts/probe_c4.py) — and writes them straight into the owning
+        // lane's LDS window; chunks 4.. are loaded per lane.  C4, 2^20 records, same box: pipelined
+        // 78 vs 82 us/step (all columns), 52 vs 55 (chain); isolated status-only 64 vs 70 us
+        // (profiles/ab/r02p_c4_coop_windows.txt).
+        off = 0;
+        len = 0;
+        if (act) packet_range(p, base + threadIdx.x, off, len);
+        const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
+        const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; k++) {
+            const uint32_t r = 16u * k + (wl >> 2), c = wl & 3u;
+            const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                                  (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+            uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
+            a = a > last16 ? last16 : a;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
+            uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
+        }
+#pragma unroll
+        for (int c = 4; c < NCH; c++) {
+            uint64_t a = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
+            a = a > last16 ? last16 : a;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
+            uint32_t* w = reinterpret_cast<uint32_t*>(lds + threadIdx.x * lane_stride(NCH)) + 4 * c;
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act);
+        return;
+    }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM, WK>(p, lds, S, base, chunk, off, len, act);
+    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act);
 }
 
-template <int NCH, uint32_t GM, int WK>
+template <int NCH, uint32_t GM, int WK, bool STAGED>
 #ifndef PKTGPU_FAST_REG
 // 1: waves whose packets all take the fast path decode from registers, no LDS.  0 (default):
 // they stage and emit through LDS like mixed waves.  C2, same box: registers 28.7 us isolated /
 // 24.0 us pipelined per step, LDS 29.8 / 23.4 — the pipelined rate is the bench's value.
 #define PKTGPU_FAST_REG 0
 #endif
-__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortLds& S, uint32_t base,
+__device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own) {
     const uint32_t t = threadIdx.x;
@@ -317,9 +331,8 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
     // loaded registers decide its whole chain: it skips the walk.
     bool fast = false, fudp = false;
     uint32_t fv = 0;
-    if constexpr (NCH >= 4) {
-        // (not with the sorted path: a lane there walks another lane's staged packet)
-        if (p.fast && !p.sort && active_own && (off_own & 15) == 0) {
+    if constexpr (NCH >= 4 && !STAGED) {
+        if (p.fast && active_own && (off_own & 15) == 0) {
             const uint32_t e0 = chunk[0].w & 0xFFFFu, e1 = chunk[1].x & 0xFFFFu, e2 = chunk[1].y & 0xFFFFu;
             const bool v0 = e0 == 0x0008u;                    // little-endian 0x0800
             const bool v1 = e0 == 0x0081u && e1 == 0x0008u;   // 0x8100, 0x0800
@@ -364,8 +377,8 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
         push(1 + v, PKT_HDR_IPV4, 14u + 4u * v);
         push(2 + v, fudp ? PKT_HDR_UDP : PKT_HDR_TCP, l4);
     };
-    if constexpr (NCH >= 4) {
-        if (PKTGPU_FAST_REG && !p.sort && __ballot(fast && fv == 0) == __ballot(active_own)) {
+    if constexpr (NCH >= 4 && !STAGED) {
+        if (PKTGPU_FAST_REG && __ballot(fast && fv == 0) == __ballot(active_own)) {
             if (!active_own) return;
             RegView<NCH> rv;
 #pragma unroll
@@ -382,94 +395,18 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, SortL
             return;
         }
     }
-    stage_window<NCH>(lds, t, chunk);
-    const PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
+    if constexpr (!STAGED) stage_window<NCH>(lds, t, chunk);
+    PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
 
-    if (!p.sort) {
-        // ---- unsorted: each lane walks and emits its own packet (no barrier: own LDS only)
-        __builtin_amdgcn_wave_barrier();
-        WalkResult r;
-        walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r);
-        if constexpr (NCH >= 4) {
-            if (fast) fast_result(r, fv);
-        }
-        if (!active_own) return;
-        emit_chain<GM>(out, i_own, len_own, r);
-        emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
-        return;
-    }
-
-    // ---- sorted: counting sort of the block's packets by chain class (LDS atomics give each
-    // lane its rank in its bucket; wave 0 scans the 64 bucket counts), walk in sorted order so a
-    // wave holds one layout, stage the walk results in LDS, then every lane emits its OWN packet
-    // (coalesced stores at the packets' own indices).
-    const uint32_t key = class_key(pv_own, active_own);
-    if (t < 64) S.hist[t] = 0;
-    if (t == 0) { S.key0 = key; S.mixed = 0; }
-    __syncthreads();
-    if (key != S.key0) S.mixed = 1;
-    const uint32_t rank = atomicAdd(&S.hist[key], 1u);
-    __syncthreads();
-    uint32_t q = t;
-    if (S.mixed) {  // block-uniform
-        if (t < 64) {
-            const uint32_t v = S.hist[t];
-            uint32_t x = v;
-#pragma unroll
-            for (int d = 1; d < 64; d <<= 1) {
-                const uint32_t y = __shfl_up(x, d, 64);
-                if ((int)t >= d) x += y;
-            }
-            S.hist[t] = x - v;
-        }
-        __syncthreads();
-        S.perm[S.hist[key] + rank] = (uint16_t)t;
-        __syncthreads();
-        q = S.perm[t];
-    }
-    {
-        const uint32_t iq = base + q;
-        const bool aq = iq < p.n;
-        uint64_t offq = 0;
-        uint32_t lenq = 0;
-        if (aq) packet_range(p, iq, offq, lenq);
-        const PacketView pvq = make_view(p, lds, q, offq, lenq, NCH);
-        auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
-            S.slot_type[slot][q] = (uint8_t)ty;
-            S.slot_off[slot][q] = (uint16_t)o;
-        };
-        WalkResult r;
-        walk<WK>(pvq, entry_state(p.entry), aq, push, r);
-        S.status[q] = (uint8_t)r.status;
-        S.n[q] = (uint8_t)r.n;
-        S.poff[q] = (uint16_t)r.payload_off;
-        S.mask[q] = r.mask;
-        S.first[0][q] = (int16_t)r.f_eth;
-        S.first[1][q] = (int16_t)r.f_vlan;
-        S.first[2][q] = (int16_t)r.f_ipv4;
-        S.first[3][q] = (int16_t)r.f_ipv6;
-        S.first[4][q] = (int16_t)r.f_tcp;
-        S.first[5][q] = (int16_t)r.f_udp;
-    }
-    __syncthreads();
-    if (!active_own) return;
+    // each lane walks and emits its own packet (no barrier: own LDS only)
+    __builtin_amdgcn_wave_barrier();
     WalkResult r;
-    r.status = S.status[t];
-    r.n = S.n[t];
-    r.payload_off = S.poff[t];
-    r.mask = S.mask[t];
-    r.f_eth = S.first[0][t];
-    r.f_vlan = S.first[1][t];
-    r.f_ipv4 = S.first[2][t];
-    r.f_ipv6 = S.first[3][t];
-    r.f_tcp = S.first[4][t];
-    r.f_udp = S.first[5][t];
-    if (want<GM, G_CHAIN>(out.hdr_type) || want<GM, G_CHAIN>(out.hdr_off)) {
-        for (uint32_t j = 0; j < r.n; j++) {
-            if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)j * ns + i_own] = S.slot_type[j][t];
-            if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)j * ns + i_own] = S.slot_off[j][t];
-        }
+    walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r,
+             reinterpret_cast<uint16_t*>(lds + window_lds(NCH)) + t, (uint32_t)kBlock);
+    if constexpr (NCH >= 4) {
+        if (fast) fast_result(r, fv);
     }
+    if (!active_own) return;
     emit_chain<GM>(out, i_own, len_own, r);
     emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
 }
@@ -535,6 +472,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
         pv.off = off;
         pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
         pv.shift = rel & 3u;
+        pv.win_lo = 0;
         pv.win_end = (npiece << 10) - rel;  // >= len: the whole record is in LDS
         pv.len = len;
     } else {
@@ -556,7 +494,8 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
         if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
     };
     WalkResult r;
-    walk<WK>(pv, entry_state(p.entry), active, push, r);
+    walk<WK>(pv, entry_state(p.entry), active, push, r, reinterpret_cast<uint16_t*>(lds + span_region(NCH)) + lane,
+             kSpanBlock);
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
@@ -570,9 +509,9 @@ template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
-                           dim3(kSpanBlock), span_region(NCH), s, kp);
+                           dim3(kSpanBlock), span_region(NCH) + (WK ? first_lds(kSpanBlock) : 0), s, kp);
     } else {
-        const size_t lds = window_lds(NCH) + (kp.sort ? sizeof(SortLds) : 0);
+        const size_t lds = window_lds(NCH) + (WK ? first_lds(kBlock) : 0);
         hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }
@@ -672,7 +611,6 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
     pkt_ctx* c = new pkt_ctx();
     c->device = device;
     c->window = 0;
-    c->sort = 0;
     c->fast = 1;
     c->staging = 0;
     c->walk = 0;
@@ -728,12 +666,6 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
     return PKT_SUCCESS;
 }
 
-int pkt_ctx_set_sort(pkt_ctx_t* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
-    ctx->sort = mode;
-    return PKT_SUCCESS;
-}
-
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                       void* stream, uint64_t off_bias, int staging);
 
@@ -774,9 +706,9 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     group_masks(*out, full, any);
     const uint32_t gm = (full == any) ? full : G_RUNTIME;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    // Staging: wave spans when asked (not with the sorted path); per-lane windows otherwise
-    // (auto: spans measured slower on C3 and C4).
-    const int mode = (staging == 2 && ctx->sort != 1) ? M_SPAN : M_TILE;
+    // Staging: wave spans when asked; per-lane windows otherwise (auto: spans measured slower on
+    // device-resident C3 and C4).
+    const int mode = staging == 2 ? M_SPAN : M_TILE;
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
@@ -793,8 +725,6 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         kp.stride = b->stride;
         kp.n = (uint32_t)cnt;
         kp.entry = entry;
-        // auto = off: the sorted path measured slower on C3 and C4
-        kp.sort = ctx->sort == 1;
         kp.fast = ctx->fast && (entry == PKT_ENTRY_PARSE || entry == PKT_ENTRY_ETHERNET);
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);

@@ -46,7 +46,6 @@ struct pkt_ctx {
     HostPipe hp;
     PcapScratch pc;
     uint32_t window;  // 0 = auto
-    int sort;         // 0 = auto (indexed batches), 1 = always, 2 = never
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep

@@ -56,7 +56,6 @@ struct KParams {
     uint32_t stride;
     uint32_t n;
     int entry;
-    int sort;  // in-block counting sort by chain class before the walk
     int fast;  // register fast path for Ether/IPv4/UDP|TCP (entries PARSE / ETHERNET)
     pkt_out_t out;
 };
@@ -100,8 +99,9 @@ struct PacketView {
     const uint8_t* slab;      // slab base (16-byte aligned)
     uint64_t off;             // packet start in the slab
     uint64_t last4;           // last readable aligned dword offset of the slab
-    uint32_t shift;           // packet start - aligned window start (0..15)
-    uint32_t win_end;         // packet bytes [0, win_end) are in the window
+    uint32_t shift;           // LDS byte of packet byte b = b + shift (mod 2^32: "negative" after a slide)
+    uint32_t win_lo;          // packet bytes [win_lo, win_end) are in the window (win_lo > 0 only
+    uint32_t win_end;         //   after the lockstep walk slid the window forward)
     uint32_t len;             // packet length
 
     // aligned dword k of the window
@@ -117,7 +117,7 @@ struct PacketView {
     // n (1..4) bytes at packet offset b, little-endian in the low bytes (garbage above n).
     // Caller guarantees b + n <= len.  Bytes past the window come from global memory (L2).
     __device__ __forceinline__ uint32_t le(uint32_t b, uint32_t n) const {
-        if (b + n <= win_end) {
+        if (b >= win_lo && b + n <= win_end) {
             uint32_t wb = b + shift;
             uint32_t k = wb >> 2, sh = wb & 3;
             uint32_t lo = wdw(k);
@@ -140,7 +140,7 @@ struct PacketView {
         (void)nbytes;
         uint32_t a[NW + 1];
         uint32_t sh;
-        if (b + 4 * NW <= win_end) {
+        if (b >= win_lo && b + 4 * NW <= win_end) {
             const uint32_t wb = b + shift;
             const uint32_t k = wb >> 2;
             sh = wb & 3;
@@ -338,36 +338,31 @@ __device__ __forceinline__ uint32_t tab6(uint64_t lo, uint64_t hi, uint32_t st) 
     return (uint32_t)(t >> (6u * (h ? st - 10u : st))) & 63u;
 }
 
-// rec() with a run-time type
+// One lockstep iteration for every live lane: the header of the lane's state is checked, read and
+// recorded with the state kept in a few registers and the checks folded into one failure code (no
+// early returns: a branchy form made the compiler copy the whole lane state at every exit).  Only
+// GRE options and the ERSPAN3 platform header take a branch, taken when a lane needs it.
+// Semantics are exactly step<S>'s: same checks in the same order, same records.  The first offset
+// of each type 1..7 goes to the lane's LDS slot fl[type * fs] when the type is first recorded.
+struct LockLane {
+    uint32_t st, o, n, mask, status, pay, steps;
+    bool live;
+};
+
 template <class Push>
-__device__ __forceinline__ void rec_rt(Lane& L, uint32_t t, uint32_t off, Push& push) {
-    push(L.r.n, t, off);
-    L.r.n++;
-    L.r.mask |= 1u << t;
-    const int32_t o = (int32_t)off;
-    if (t == PKT_HDR_ETHER && L.r.f_eth < 0) L.r.f_eth = o;
-    if (t == PKT_HDR_VLAN && L.r.f_vlan < 0) L.r.f_vlan = o;
-    if (t == PKT_HDR_IPV4 && L.r.f_ipv4 < 0) L.r.f_ipv4 = o;
-    if (t == PKT_HDR_IPV6 && L.r.f_ipv6 < 0) L.r.f_ipv6 = o;
-    if (t == PKT_HDR_TCP && L.r.f_tcp < 0) L.r.f_tcp = o;
-    if (t == PKT_HDR_UDP && L.r.f_udp < 0) L.r.f_udp = o;
+__device__ __forceinline__ void lrec(LockLane& L, uint32_t t, uint32_t off, Push& push, uint16_t* fl, uint32_t fs) {
+    push(L.n, t, off);
+    if (t <= PKT_HDR_UDP && !((L.mask >> t) & 1u)) fl[t * fs] = (uint16_t)off;
+    L.mask |= 1u << t;
+    L.n++;
 }
 
 template <class Push>
-__device__ __forceinline__ void gstep(Lane& L, const PacketView& pv, Push& push) {
-    const uint32_t st = L.st, o = L.o, len = pv.len;
-    if (st == S_ACCEPT) {  // fast.rs:223-227
-        L.r.payload_off = o;
-        L.live = false;
-        return;
-    }
+__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push, uint16_t* fl, uint32_t fs) {
+    const uint32_t st = L.st, o = L.o;
+    L.steps++;
     const uint32_t sz = tab6(kSz0, kSz1, st);
-    if (o + sz > len) { fail(L, PKT_TRUNCATED); return; }  // `&arr[0..X::size()]` (PARSE: arr[12..13])
-    if (st != S_PARSE && L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
-    // the dispatch dword (bytes past the header are read but never used)
-    const uint32_t D = bswap32(pv.le(o + tab6(kDw0, kDw1, st), 4));
     const uint32_t hw = D >> 16;
-    // next state of every kind, then the one for this state
     const uint32_t et_next = etype_next(hw);
     const bool v6 = st == S_IPV6;
     const uint32_t ip_next = ipproto_next(v6 ? (D >> 8) & 0xFFu : hw & 0xFFu, v6);
@@ -382,43 +377,49 @@ __device__ __forceinline__ void gstep(Lane& L, const PacketView& pv, Push& push)
     nx = (st == S_GRE) ? gre_next(D & 0xFFFFu) : nx;
     nx = (st == S_ERSPAN2 || st == S_ERSPAN3 || st == S_VXLAN) ? S_ETHER : nx;
     nx = (st == S_UDP) ? (hw == 4789u ? S_VXLAN : S_ACCEPT) : nx;
-    if (st == S_PARSE) {
-        L.st = nx;
-        return;
+    // the reference's panics in its order: iteration bound (walk), `&arr[0..X::size()]`, depth,
+    // parse_mpls_bos's arr[4] (fast.rs:74-83, Q3); accept ends the walk (fast.rs:223-227)
+    const bool acc = st == S_ACCEPT;
+    uint32_t f = 0;
+    f = (st == S_MPLS_BOS && o + 5 > len) ? (uint32_t)PKT_TRUNCATED : f;
+    f = (st != S_PARSE && L.n >= PKT_MAX_HDRS) ? (uint32_t)PKT_DEPTH_LIMIT : f;
+    f = (o + sz > len) ? (uint32_t)PKT_TRUNCATED : f;
+    f = acc ? 0u : f;
+    f = (L.steps > PKT_MAX_HDRS + 3) ? (uint32_t)PKT_DEPTH_LIMIT : f;
+    const bool go = f == 0 && !acc;
+    uint32_t q = o;
+    if (go && st != S_PARSE) {
+        lrec(L, tab6(kTy0, kTy1, st), o, push, fl, fs);
+        q = o + sz;
+        const bool gopt = st == S_GRE && (D & 0xB0000000u) != 0;
+        const bool plat = st == S_ERSPAN3 && (D & 1u);
+        if (gopt) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
+            const uint32_t c = D >> 31, k = (D >> 29) & 1u, sb = (D >> 28) & 1u;
+            if (c) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+            const uint32_t oc = q;
+            q += 4u * c;
+            if (!f && k) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+            const uint32_t okey = q;
+            q += 4u * k;
+            if (!f && sb) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c + k >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+            const uint32_t oseq = q;
+            q += 4u * sb;
+            if (!f) {
+                if (sb) lrec(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push, fl, fs);
+                if (k) lrec(L, PKT_HDR_GRE_KEY, okey, push, fl, fs);
+                if (c) lrec(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push, fl, fs);
+            }
+        } else if (plat) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
+            f = (q + 8 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+            if (!f) {
+                lrec(L, PKT_HDR_ERSPAN_PLATFORM, q, push, fl, fs);
+                q += 8;
+            }
+        }
     }
-    // fast.rs:74-83: arr[MPLS::size()] must exist (Q3)
-    if (st == S_MPLS_BOS && o + 5 > len) { fail(L, PKT_TRUNCATED); return; }
-    rec_rt(L, tab6(kTy0, kTy1, st), o, push);
-    uint32_t q = o + sz;
-    if (st == S_GRE) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
-        const uint32_t c = D >> 31, k = (D >> 29) & 1u, sb = (D >> 28) & 1u;
-        if (c) {
-            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
-            if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
-        }
-        const uint32_t oc = q;
-        q += 4u * c;
-        if (k) {
-            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
-            if (L.r.n + c >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
-        }
-        const uint32_t okey = q;
-        q += 4u * k;
-        if (sb) {
-            if (q + 4 > len) { fail(L, PKT_TRUNCATED); return; }
-            if (L.r.n + c + k >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
-        }
-        const uint32_t oseq = q;
-        q += 4u * sb;
-        if (sb) rec_rt(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push);
-        if (k) rec_rt(L, PKT_HDR_GRE_KEY, okey, push);
-        if (c) rec_rt(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push);
-    } else if (st == S_ERSPAN3 && (D & 1u)) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
-        if (q + 8 > len) { fail(L, PKT_TRUNCATED); return; }
-        if (L.r.n >= PKT_MAX_HDRS) { fail(L, PKT_DEPTH_LIMIT); return; }
-        rec_rt(L, PKT_HDR_ERSPAN_PLATFORM, q, push);
-        q += 8;
-    }
+    L.pay = (acc && f == 0) ? o : L.pay;
+    L.status = f ? f : L.status;
+    L.live = go && f == 0;
     L.o = q;
     L.st = nx;
 }
@@ -426,30 +427,47 @@ __device__ __forceinline__ void gstep(Lane& L, const PacketView& pv, Push& push)
 // The walk.  WK = 0, waterfall: each iteration takes the state of the first live lane and every
 // live lane in that state advances one step under a SCALAR switch — a wave whose packets share a
 // layout runs exactly one case per header, a mixed wave one case per distinct (state, depth).
-// WK = 1, lockstep: every live lane advances one header per iteration through gstep() — a mixed
+// WK = 1, lockstep: every live lane advances one header per iteration through lstep() — a mixed
 // wave runs (its longest chain + 2) iterations (C4: 10 instead of ~38).
+// Lockstep extra: fl/fs = the lane's first-offset LDS slots (fl[type * fs]).  (Refilling the
+// window for headers past it, one round trip per wave instead of one dependent read per header,
+// measured slower: C4 status-only 88-90 vs 66-68 us; so did prefetching the sectors past the
+// window into L2, 78 vs 67 us — profiles/ab/r02o_c4_refill_prefetch.txt.)
 template <int WK, class Push>
-__device__ __forceinline__ void walk(const PacketView& pv, uint32_t state, bool active, Push&& push,
-                                     WalkResult& out) {
+__device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active, Push&& push,
+                                     WalkResult& out, uint16_t* fl = nullptr, uint32_t fs = 0) {
     if constexpr (WK == 1) {
-        Lane L;
-        L.st = state;
-        L.o = 0;
-        L.steps = 0;
-        L.live = active;
-        L.r.status = PKT_OK;
-        L.r.n = 0;
-        L.r.payload_off = 0;
-        L.r.mask = 0;
-        L.r.f_eth = L.r.f_vlan = L.r.f_ipv4 = L.r.f_ipv6 = L.r.f_tcp = L.r.f_udp = -1;
+        LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active};
         while (__ballot(L.live)) {
             if (L.live) {
-                // at most PKT_MAX_HDRS headers + parse + accept + the failing step
-                if (++L.steps > PKT_MAX_HDRS + 3) fail(L, PKT_DEPTH_LIMIT);
-                else gstep(L, pv, push);
+                // the dispatch dword of this step (big-endian; bytes past the header are read but
+                // never used): from the window when it holds it, else from global memory — and
+                // only if the step gets past its iteration and slice checks
+                const uint32_t b = L.o + tab6(kDw0, kDw1, L.st);
+                const bool want = L.st != S_ACCEPT && L.steps < PKT_MAX_HDRS + 3 &&
+                                  L.o + tab6(kSz0, kSz1, L.st) <= pv.len;
+                uint32_t D = 0;
+                if (b >= pv.win_lo && b + 4 <= pv.win_end) {
+                    const uint32_t wb = b + pv.shift, k = wb >> 2, sh = wb & 3;
+                    const uint32_t* w = reinterpret_cast<const uint32_t*>(pv.lw);
+                    D = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+                } else if (want) {
+                    D = pv.le(b, 4);
+                }
+                lstep(L, pv.len, bswap32(D), push, fl, fs);
             }
         }
-        out = L.r;
+        out.status = L.status;
+        out.n = L.n;
+        out.payload_off = L.pay;
+        out.mask = L.mask;
+        const uint32_t m = L.status == PKT_OK ? L.mask : 0u;
+        out.f_eth = (m >> PKT_HDR_ETHER) & 1u ? (int32_t)fl[PKT_HDR_ETHER * fs] : -1;
+        out.f_vlan = (m >> PKT_HDR_VLAN) & 1u ? (int32_t)fl[PKT_HDR_VLAN * fs] : -1;
+        out.f_ipv4 = (m >> PKT_HDR_IPV4) & 1u ? (int32_t)fl[PKT_HDR_IPV4 * fs] : -1;
+        out.f_ipv6 = (m >> PKT_HDR_IPV6) & 1u ? (int32_t)fl[PKT_HDR_IPV6 * fs] : -1;
+        out.f_tcp = (m >> PKT_HDR_TCP) & 1u ? (int32_t)fl[PKT_HDR_TCP * fs] : -1;
+        out.f_udp = (m >> PKT_HDR_UDP) & 1u ? (int32_t)fl[PKT_HDR_UDP * fs] : -1;
         return;
     }
     Lane L;

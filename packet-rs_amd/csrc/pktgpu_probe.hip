@@ -110,3 +110,33 @@ extern "C" int pkt_probe_fetch(const uint8_t* buf, uint64_t buf_len, uint32_t n,
                        n, stride, phase, width, out);
     return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
 }
+
+// pkt_probe_c4load: the load shape of the indexed-batch parse without the walk.  Lane i loads `nch`
+// 16-byte chunks from offsets[i] rounded down to 2^align_log2 bytes (clamped to the slab) and writes
+// one byte.  Its time per launch is what the window loads alone cost for a given window placement.
+namespace {
+__global__ __launch_bounds__(256) void c4load_kernel(const uint8_t* slab, uint64_t slab_len, const uint64_t* offs,
+                                                     uint32_t n, uint32_t nch, uint32_t align_log2, uint8_t* out) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint64_t last16 = ((slab_len + 15) & ~(uint64_t)15) - 16;
+    const uint64_t a0 = offs[i] & ~((1ull << align_log2) - 1ull);
+    uint32_t acc = 0;
+    for (uint32_t c = 0; c < nch; c++) {
+        uint64_t a = a0 + 16u * c;
+        a = a > last16 ? last16 : a;
+        const uint4 v = *reinterpret_cast<const uint4*>(slab + a);
+        acc ^= v.x + v.y * 3u + v.z * 5u + v.w * 7u;
+    }
+    out[i] = (uint8_t)acc;
+}
+}  // namespace
+
+extern "C" int pkt_probe_c4load(const uint8_t* slab, uint64_t slab_len, const uint64_t* offs, uint32_t n, uint32_t nch,
+                                uint32_t align_log2, uint8_t* out, void* stream) {
+    if (!slab || !offs || !out || !n || slab_len < 16 || align_log2 < 4 || align_log2 > 8 || nch == 0 || nch > 32)
+        return PKT_ERR_INVALID_ARG;
+    hipLaunchKernelGGL(c4load_kernel, dim3((n + 255) / 256), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), slab,
+                       slab_len, offs, n, nch, align_log2, out);
+    return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
+}

@@ -130,6 +130,7 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     pv.off = off;
     pv.last4 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 4;
     pv.shift = (uint32_t)(off & 15);
+    pv.win_lo = 0;
     pv.win_end = 16u * kXnch - pv.shift;
     pv.len = 0xFFFFFFFFu;  // (le() does not use it)
     __builtin_amdgcn_wave_barrier();

@@ -109,10 +109,6 @@ class Parser:
         """0 = auto, 1 = waterfall, 2 = lockstep (pkt_ctx_set_walk)."""
         self._check(self._L.pkt_ctx_set_walk(self._ctx, int(mode)), "pkt_ctx_set_walk")
 
-    def set_sort(self, mode):
-        """0 = auto (indexed batches), 1 = always, 2 = never (see pkt_ctx_set_sort)."""
-        self._check(self._L.pkt_ctx_set_sort(self._ctx, int(mode)), "pkt_ctx_set_sort")
-
     def _check(self, rc, what):
         if rc != 0:
             msg = self._L.pkt_ctx_last_error(self._ctx)

@@ -60,7 +60,6 @@ SIGNATURES = {
     "pkt_ctx_destroy": (ctypes.c_int, [_P]),
     "pkt_ctx_last_error": (ctypes.c_char_p, [_P]),
     "pkt_ctx_set_window": (ctypes.c_int, [_P, ctypes.c_uint32]),
-    "pkt_ctx_set_sort": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_fastpath": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_staging": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_walk": (ctypes.c_int, [_P, ctypes.c_int]),

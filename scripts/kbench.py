@@ -22,13 +22,11 @@ ap.add_argument("--iters", type=int, default=32)
 ap.add_argument("--variants", default="status;chain;chain,ether,ipv4,udp;all")
 ap.add_argument("--windows", default="0")
 ap.add_argument("--streams", default="1")
-ap.add_argument("--sort", type=int, default=0, help="pkt_ctx_set_sort mode")
 ap.add_argument("--staging", type=int, default=0, help="pkt_ctx_set_staging mode")
 args = ap.parse_args()
 
 dev = torch.device("cuda", 0)
 P = pktgpu.Parser(0)
-P.set_sort(args.sort)
 P.set_staging(args.staging)
 n = args.n
 if args.config == "c2":

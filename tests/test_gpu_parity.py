@@ -400,32 +400,28 @@ def test_to_vec_c4_dst_layouts_vs_oracle(P, shift):
     assert (o[mask] == 0xEE).all()
 
 
-# ------------------------------------------------------------------ in-block steering (sort)
-@pytest.mark.parametrize("mode", [1, 2])
-def test_sort_modes_bit_exact(P, mode):
-    """Forcing the in-block class sort on (1) / off (2) changes nothing in the output."""
-    P.set_sort(mode)
-    try:
-        pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
-        offs, lens = gen.pcap_index_py(pc)
-        both(P, np.frombuffer(pc, np.uint8), 22, offsets=offs, lens=lens, label=f"ref22 s{mode}")
-        buf, offs, lens = gen.gen_c4(50000, seed=41)
-        both(P, buf, len(offs), offsets=offs, lens=lens, label=f"c4 s{mode}")
-        slab = gen.gen_c3(50001, seed=42)
-        both(P, slab, 50001, stride=128, label=f"c3 s{mode}")
-        slab = gen.gen_c2(4099, seed=43)
-        both(P, slab, 4099, stride=64, label=f"c2 s{mode}")
-        rng = np.random.default_rng(44)
-        pk = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes() for _ in range(5000)]
-        pk += [p.to_vec()[:int(rng.integers(10, 120))] for p in gen.reference_22_packets() for _ in range(50)]
-        b = b"".join(pk)
-        ln = np.array([len(x) for x in pk], np.uint32)
-        of = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
-        for entry in ("parse", "parse_ethernet", "parse_ipv4"):
-            both(P, np.frombuffer(b + bytes(16), np.uint8), len(pk), offsets=of, lens=ln, entry=entry,
-                 label=f"mix {entry} s{mode}")
-    finally:
-        P.set_sort(0)
+# ------------------------------------------------------------------ mixed inputs
+def test_mixed_inputs_bit_exact(P):
+    """The reference pcap, a C4 replay, C3/C2 slabs and random/truncated records under three
+    entries: every column equals the oracle."""
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    offs, lens = gen.pcap_index_py(pc)
+    both(P, np.frombuffer(pc, np.uint8), 22, offsets=offs, lens=lens, label="ref22")
+    buf, offs, lens = gen.gen_c4(50000, seed=41)
+    both(P, buf, len(offs), offsets=offs, lens=lens, label="c4")
+    slab = gen.gen_c3(50001, seed=42)
+    both(P, slab, 50001, stride=128, label="c3")
+    slab = gen.gen_c2(4099, seed=43)
+    both(P, slab, 4099, stride=64, label="c2")
+    rng = np.random.default_rng(44)
+    pk = [rng.integers(0, 256, int(rng.integers(0, 90)), dtype=np.uint8).tobytes() for _ in range(5000)]
+    pk += [p.to_vec()[:int(rng.integers(10, 120))] for p in gen.reference_22_packets() for _ in range(50)]
+    b = b"".join(pk)
+    ln = np.array([len(x) for x in pk], np.uint32)
+    of = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
+    for entry in ("parse", "parse_ethernet", "parse_ipv4"):
+        both(P, np.frombuffer(b + bytes(16), np.uint8), len(pk), offsets=of, lens=ln, entry=entry,
+             label=f"mix {entry}")
 
 
 # ------------------------------------------------------------------ register fast path
