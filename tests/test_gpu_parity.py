@@ -529,6 +529,32 @@ def test_staging_modes_bit_exact(P, staging):
         P.set_window(0)
 
 
+@pytest.mark.parametrize("staging", [0, 2])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 65537])
+def test_indexed_sizes_and_wide_ranges(P, n, staging):
+    """Indexed batches around the wave / block sizes, with jumbo records (wave ranges past the
+    span staging's 16 KiB: its per-lane fallback) mixed with tiny, empty and truncated ones."""
+    rng = np.random.default_rng(n)
+    tm = [p.to_vec() for p in gen.reference_22_packets()]
+    pk = []
+    for k in range(n):
+        u = rng.random()
+        if u < 0.02:
+            pk.append(tm[int(rng.integers(0, 22))] + bytes(int(rng.integers(1000, 9000))))  # jumbo
+        elif u < 0.04:
+            pk.append(tm[int(rng.integers(0, 22))][:int(rng.integers(0, 40))])               # truncated
+        else:
+            pk.append(tm[int(rng.integers(0, 22))])
+    buf = gen.pcap_bytes(pk)
+    offs, lens = gen.pcap_index_py(buf)
+    P.set_staging(staging)
+    try:
+        both(P, np.frombuffer(buf, np.uint8), n, offsets=offs, lens=lens, label=f"st{staging} n={n}")
+        both(P, np.frombuffer(buf, np.uint8), n, offsets=offs, lens=lens, columns=["chain"], label=f"st{staging} chain n={n}")
+    finally:
+        P.set_staging(0)
+
+
 @pytest.mark.parametrize("walk", [1, 2])
 def test_walk_modes_bit_exact(P, walk):
     """Waterfall (1) and lockstep (2) walks give identical columns on every mix, every entry,
