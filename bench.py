@@ -126,6 +126,18 @@ def algorithmic_bytes(n, cols, n_slots, span):
     return read, written
 
 
+def line_bytes(n, stride, offs, span):
+    """Bytes of the distinct 128-byte lines (the HBM fetch granule on gfx950) that
+    hold the packets' header bytes [start, start + span): what any kernel must read at least."""
+    span = np.maximum(span.astype(np.int64), 1)
+    start = offs.astype(np.int64) if offs is not None else np.arange(n, dtype=np.int64) * stride
+    first, last = start // 128, (start + span - 1) // 128
+    order = np.argsort(first, kind="stable")
+    first, last = first[order], last[order]
+    prev = np.concatenate(([np.int64(-1)], np.maximum.accumulate(last)[:-1]))
+    return int(np.maximum(last - np.maximum(first, prev + 1) + 1, 0).sum()) * 128
+
+
 # ------------------------------------------------------------------------------ CPU baseline
 def host_cores():
     """Cores this process may run on: its affinity set, capped by a cgroup CPU quota if any."""
@@ -403,11 +415,20 @@ def main():
         if rc != 0:
             raise RuntimeError(f"pkt_probe_ceiling failed ({rc})")
 
-    kern, ceil_ = [], []
+    # the practical HBM rate of this box: a device copy of the slab (read + write), same ring
+    copy_dst = torch.empty_like(d_first)
+
+    def copy_launch(k, s):
+        with torch.cuda.stream(s):
+            copy_dst.copy_(slabs[k % ring])
+
+    kern, ceil_, copy_ = [], [], []
     for _ in range(5):
         kern.append(event_avg_ms(torch, rs, parse_launch, R))
         if probe is not None:
             ceil_.append(event_avg_ms(torch, rs, probe_launch, R))
+        copy_.append(event_avg_ms(torch, rs, copy_launch, R))
+    del copy_dst
     # the probe overwrote output sets: re-parse them so the last step's columns are real
     for r in range(ring):
         parse_launch(r, rs)
@@ -483,6 +504,19 @@ def main():
             "avg_kernel_us": round(cs * 1e6, 3), "achieved": round(algo / cs / 1e9, 2),
             "frac_of_peak": round(algo / cs / 1e9 / HBM_PEAK_GBS, 4),
             "parse_frac_of_ceiling": round(cs / avg_kern_s, 4)}
+    # the line-granular floor: distinct 128-B lines holding header bytes + the batch index read
+    # + the columns written, priced at this box's measured copy rate
+    idx_b = 12 * n if offs_np is not None else 0
+    floor_b = line_bytes(n, stride, offs_np, span) + idx_b + write_b
+    copy_gbs = 2 * slab_bytes / (float(np.median(copy_)) * 1e-3) / 1e9
+    floor_s = floor_b / (copy_gbs * 1e9)
+    res["roofline"]["line_floor"] = {
+        "bytes_per_launch": floor_b, "read_lines": floor_b - idx_b - write_b, "index_read": idx_b,
+        "written": write_b, "copy_rate_GBps": round(copy_gbs, 2),
+        "copy": "torch copy_ of the slab over the same ring (read + write), HIP events, one stream",
+        "floor_us_at_copy_rate": round(floor_s * 1e6, 3),
+        "kernel_frac_of_floor": round(floor_s / avg_kern_s, 4),
+        "pipelined_frac_of_floor": round(floor_s / pipe_s, 4)}
     # HBM traffic per launch from the committed rocprofv3 PMC passes of this config, if any
     tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
     if os.path.exists(tpath) and args.columns == default_cols and n == 1 << 20:

@@ -254,6 +254,9 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
 #ifndef PKTGPU_WAVES_PER_EU
 #define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
 #endif
+#ifndef PKTGPU_COOP_FIXED
+#define PKTGPU_COOP_FIXED 1  // fixed-stride batches load their windows cooperatively too
+#endif
 template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
 void parse_kernel(KParams p) {
@@ -263,14 +266,16 @@ void parse_kernel(KParams p) {
     u32x4 chunk[NCH];
     uint64_t off;
     uint32_t len;
-    if constexpr (WK == 1 && NCH >= 4) {
-        // Indexed batches: the wave loads its 64 windows cooperatively — in load k, lanes 4j..4j+3
+    if constexpr (NCH >= 4 && (WK == 1 || PKTGPU_COOP_FIXED)) {
+        // The wave loads its 64 windows cooperatively — in load k, lanes 4j..4j+3
         // fetch chunks 0-3 of packet 16k + j, i.e. 64 contiguous bytes per 4 lanes instead of one
         // scattered 16-byte piece per lane (the per-lane shape is request-bound: 42 us for the
         // 2^20 C4 windows alone, scripts/probe_c4.py) — and writes them straight into the owning
         // lane's LDS window; chunks 4.. are loaded per lane.  C4, 2^20 records, same box: pipelined
         // 78 vs 82 us/step (all columns), 52 vs 55 (chain); isolated status-only 64 vs 70 us
-        // (profiles/ab/r02p_c4_coop_windows.txt).
+        // (profiles/ab/r02p_c4_coop_windows.txt).  Fixed-stride batches the same way (the fast
+        // path then classifies from the lane's LDS window): C2 pipelined 23.9 vs 25.2 us/step, C3
+        // 43.3 vs 46.1 (profiles/ab/r02x_coop_fixed_stride.txt).
         off = 0;
         len = 0;
         if (act) packet_range(p, base + threadIdx.x, off, len);
@@ -331,15 +336,25 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     // loaded registers decide its whole chain: it skips the walk.
     bool fast = false, fudp = false;
     uint32_t fv = 0;
-    if constexpr (NCH >= 4 && !STAGED) {
+    if constexpr (NCH >= 4) {
         if (p.fast && active_own && (off_own & 15) == 0) {
-            const uint32_t e0 = chunk[0].w & 0xFFFFu, e1 = chunk[1].x & 0xFFFFu, e2 = chunk[1].y & 0xFFFFu;
+            // dwords 3..11 of the packet (little-endian), from the registers or, when the wave
+            // loaded its windows cooperatively, from the lane's own LDS window
+            uint32_t d3, d4, d5, d6, d7, d9, d10, d11;
+            if constexpr (STAGED) {
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + t * lane_stride(NCH));
+                d3 = w[3], d4 = w[4], d5 = w[5], d6 = w[6], d7 = w[7], d9 = w[9], d10 = w[10], d11 = w[11];
+            } else {
+                d3 = chunk[0].w, d4 = chunk[1].x, d5 = chunk[1].y, d6 = chunk[1].z, d7 = chunk[1].w;
+                d9 = chunk[2].y, d10 = chunk[2].z, d11 = chunk[2].w;
+            }
+            const uint32_t e0 = d3 & 0xFFFFu, e1 = d4 & 0xFFFFu, e2 = d5 & 0xFFFFu;
             const bool v0 = e0 == 0x0008u;                    // little-endian 0x0800
             const bool v1 = e0 == 0x0081u && e1 == 0x0008u;   // 0x8100, 0x0800
             const bool v2 = e0 == 0x0081u && e1 == 0x0081u && e2 == 0x0008u;
             fv = v1 ? 1u : (v2 ? 2u : 0u);
-            const uint32_t proto = (v0 ? chunk[1].y : v1 ? chunk[1].z : chunk[1].w) >> 24;
-            const uint32_t dport = (v0 ? chunk[2].y : v1 ? chunk[2].z : chunk[2].w) & 0xFFFFu;
+            const uint32_t proto = (v0 ? d5 : v1 ? d6 : d7) >> 24;
+            const uint32_t dport = (v0 ? d9 : v1 ? d10 : d11) & 0xFFFFu;
             const uint32_t l4 = 34u + 4u * fv;
             fudp = proto == 17u;
             fast = (v0 || v1 || v2) && ((fudp && len_own >= l4 + 8u && dport != 0xB512u) ||
