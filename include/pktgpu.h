@@ -321,7 +321,9 @@ int pkt_to_vec_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_out_t *
  * order, on the spec's header of every packet's chain.  The low (end-start+1) bits of
  * values[s][i] go to bits [start..=end] (bits of a field wider than 64 above the value's 64
  * bits become 0, as set_bit_range shifts the u64 right once per bit).  Packets whose chain lacks
- * the header are untouched.  `values` is a HOST array of nspec DEVICE pointers ([n] each). */
+ * the header are untouched.  `values` is a HOST array of nspec DEVICE pointers ([n] each).
+ * The packets of one batch must not overlap: a packet's bytes may be stored back whole (with
+ * their values unchanged outside the fields set), never bytes outside [offset, offset + len). */
 int pkt_set_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
                    const pkt_field_spec_t *specs, uint32_t nspec, const uint64_t *const *values,
                    void *stream);

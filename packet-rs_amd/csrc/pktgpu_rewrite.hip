@@ -10,13 +10,16 @@
 //                      two or more options (Q2), so for every other packet to_vec IS the packet's bytes
 //                      [0, len) — known from hdr_mask alone (at most one GRE option type), else checked
 //                      against the slot rows.  One wave per 64 packets: lane k reads packet k's
-//                      metadata, then lane groups of G (the wave's largest packet in 16-byte chunks,
-//                      rounded up to a power of two) copy 64/G packets per pass as 16-byte chunks
-//                      (dwords shifted into place when source and destination differ in alignment).
-//                      Q2 packets take a per-byte gather through the list.
+//                      metadata; the wave's packets then form one list of 16-byte destination chunks
+//                      (a wave scan of the per-packet counts) that the lanes copy 64 at a time
+//                      (a funnel shift when source and destination differ in alignment).  Q2
+//                      packets are gathered through the list by the whole wave, one at a time.
 //   set_fields_kernel  set_bit_range (headers.rs:315-324) per spec, in spec order, in place; chain in
-//                      LDS, all specs (up to 32) in one launch; a field of <= 64 bits is read as one
-//                      16-byte window (one round trip), set by a shift and mask, its bytes stored.
+//                      LDS, all specs (up to 32) in one launch.  The wave loads its packets' first 80
+//                      bytes into LDS cooperatively, every setter whose field lies there is applied in
+//                      LDS (one shift and mask on a 16-byte piece), and the chunks holding set bytes
+//                      are stored back cooperatively, the packet's own bytes only; a packet with a
+//                      field past its window or wider than 64 bits is set in global memory instead.
 //   ipv4_update_kernel / ipv4_csum_kernel   Packet::ipv4_checksum (packet.rs:93-107, Q1 fold).
 //   broadcast_kernel   n copies of one packet (the clone step of the pktgen loop).
 #include <hip/hip_runtime.h>
@@ -179,13 +182,94 @@ struct TParams {
 __device__ __forceinline__ void put_byte(const TParams& p, uint64_t q, uint32_t v) {
     if (q < p.dst_len) p.dst[q] = (uint8_t)v;
 }
-__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t k) {
-    return ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(v >> 32), (int)k, 64) << 32) | (uint32_t)__shfl((int)(uint32_t)v, (int)k, 64);
+
+// Store the bytes [lo, hi) of the 16-byte chunk at base + ca (o = its four little-endian dwords),
+// nothing at or past `cap`: one 16-byte store when the chunk is whole, else whole dwords where
+// covered and bytes at the edges.
+__device__ __forceinline__ void store_chunk(uint8_t* base, uint64_t cap, uint64_t ca, const uint32_t (&o)[4],
+                                            uint64_t lo, uint64_t hi) {
+    if (lo == ca && hi == ca + 16 && ca + 16 <= cap) {
+        *reinterpret_cast<uint4*>(base + ca) = make_uint4(o[0], o[1], o[2], o[3]);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint64_t a = ca + 4u * j;
+        if (a >= lo && a + 4 <= hi && a + 4 <= cap) {
+            *reinterpret_cast<uint32_t*>(base + a) = o[j];
+        } else {
+#pragma unroll
+            for (int b = 0; b < 4; b++)
+                if (a + b >= lo && a + b < hi && a + b < cap) base[a + b] = (uint8_t)(o[j] >> (8 * b));
+        }
+    }
 }
 
 // GRE option header types: two or more of them in one list is the only way the list order can
 // differ from wire order (Q2, fast.rs:154-163)
 constexpr uint32_t kGreOptMask = (1u << PKT_HDR_GRE_CHKSUM_OFFSET) | (1u << PKT_HDR_GRE_SEQUENCE_NUM) | (1u << PKT_HDR_GRE_KEY);
+
+// Store the bytes [lo, hi) of a head / tail chunk (o = its dwords) below `cap`: the whole dwords
+// it covers, then at most a byte and a short at each edge (8 store instructions, not one per
+// byte); a range inside one dword goes byte by byte.
+__device__ __forceinline__ void store_edge_chunk(uint8_t* base, uint64_t cap, uint64_t ca, const uint32_t (&o)[4],
+                                                 uint64_t lo, uint64_t hi) {
+    const uint64_t u4 = (lo + 3) & ~(uint64_t)3, d4 = hi & ~(uint64_t)3;
+    if (u4 > d4) {  // within one dword
+        const uint32_t v = o[((lo - ca) >> 2) & 3];
+        for (uint64_t a = lo; a < hi; a++)
+            if (a < cap) base[a] = (uint8_t)(v >> (8 * (a & 3)));
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint64_t a = ca + 4u * j;
+        if (a >= u4 && a + 4 <= d4 && a + 4 <= cap) *reinterpret_cast<uint32_t*>(base + a) = o[j];
+    }
+    if (lo < u4) {  // head: bytes lo .. u4-1 of dword (lo - ca) / 4
+        const uint32_t v = o[((lo - ca) >> 2) & 3];
+        uint64_t a = lo;
+        if ((a & 1) && a < cap) base[a] = (uint8_t)(v >> (8 * (a & 3)));
+        a += a & 1;
+        if (a < u4 && a + 2 <= cap) *reinterpret_cast<uint16_t*>(base + a) = (uint16_t)(v >> 16);
+    }
+    if (d4 < hi) {  // tail: bytes d4 .. hi-1 of dword (d4 - ca) / 4
+        const uint32_t v = o[((d4 - ca) >> 2) & 3];
+        const uint32_t m = (uint32_t)(hi - d4);
+        if ((m & 2) && d4 + 2 <= cap) *reinterpret_cast<uint16_t*>(base + d4) = (uint16_t)v;
+        if ((m & 1) && d4 + (m & 2) < cap) base[d4 + (m & 2)] = (uint8_t)(v >> (8 * (m & 2)));
+    }
+}
+
+// The source bytes of destination chunk ca of a packet copied from s to d (dwords o): one aligned
+// load when source and destination share their alignment, else two and a funnel shift.
+__device__ __forceinline__ void load_src_chunk(const BatchRef& b, uint64_t last16, uint64_t s, uint64_t d,
+                                               uint64_t ca, uint32_t (&o)[4]) {
+    if (((s ^ d) & 15) == 0) {
+        uint64_t a = ca - d + s;
+        a = a > last16 ? last16 : a;
+        const uint4 v = *reinterpret_cast<const uint4*>(b.slab + a);
+        o[0] = v.x, o[1] = v.y, o[2] = v.z, o[3] = v.w;
+        return;
+    }
+    // source of destination byte ca: B = ca - d + s (below 0 only for bytes before the packet,
+    // which are not stored)
+    const int64_t B = (int64_t)(ca - d) + (int64_t)s;
+    const int64_t A = B & ~(int64_t)15;
+    uint64_t a0 = A < 0 ? 0 : (uint64_t)A, a1 = a0 + 16;
+    a0 = a0 > last16 ? last16 : a0;
+    a1 = a1 > last16 ? last16 : a1;
+    const uint4 v0 = *reinterpret_cast<const uint4*>(b.slab + a0);
+    const uint4 v1 = *reinterpret_cast<const uint4*>(b.slab + a1);
+    const uint32_t sh = (uint32_t)(B - A), q = sh >> 2, r = sh & 3;
+    const uint32_t x[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const uint32_t lo_w = q == 0 ? x[j] : q == 1 ? x[j + 1] : q == 2 ? x[j + 2] : x[j + 3];
+        const uint32_t hi_w = q == 0 ? x[j + 1] : q == 1 ? x[j + 2] : q == 2 ? x[j + 3] : x[j + 4];
+        o[j] = __builtin_amdgcn_alignbyte(hi_w, lo_w, r);
+    }
+}
 
 __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     const uint32_t lane = threadIdx.x & 63u;
@@ -219,66 +303,65 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
         }
         if (p.out_len) p.out_len[i] = ok ? len : 0u;
     }
-    // ---- lane groups of G = the wave's largest packet in 16-byte chunks (power of two): 64 / G
-    // packets are copied per pass, each by its own group
-    uint32_t ch = ok ? (uint32_t)(((dst & 15) + len + 15) >> 4) : 0u;
+    // ---- identity packets: the wave's packets as ONE list of 16-byte destination chunks (a
+    // packet's chunks are consecutive, packets in lane order), lane j copying chunks j, j+64, ...:
+    // a wave-instruction writes 64 consecutive chunks whatever the packet lengths (records of a
+    // capture lie back to back, so mostly 1 KiB of contiguous destination)
+    const uint32_t w = threadIdx.x >> 6;
+    __shared__ uint32_t s_pre[kRwBlock / 64][65];
+    __shared__ uint64_t s_src[kRwBlock / 64][64], s_dst[kRwBlock / 64][64];
+    __shared__ uint32_t s_len[kRwBlock / 64][64];
+    const bool flat = ok && ident && len > 0;
+    const uint32_t ch = flat ? (uint32_t)(((dst & 15) + len + 15) >> 4) : 0u;
+    uint32_t incl = ch;  // inclusive scan over the wave
 #pragma unroll
-    for (int m = 1; m < 64; m <<= 1) ch = max(ch, (uint32_t)__shfl_xor((int)ch, m, 64));
-    ch = __builtin_amdgcn_readfirstlane(ch);  // wave-uniform after the butterfly
-    if (ch == 0) return;
-    uint32_t G = 1;
-    while (G < ch && G < 64u) G <<= 1;
-    const uint32_t per = 64u / G, sub = lane & (G - 1u);
-    for (uint32_t k0 = 0; k0 < 64u; k0 += per) {  // uniform
-        const uint32_t k = k0 + lane / G;
-        const uint64_t s = shfl64(src, k), d = shfl64(dst, k);
-        const uint32_t L = (uint32_t)__shfl((int)len, (int)k, 64);
-        const uint32_t okk = (uint32_t)__shfl((int)ok, (int)k, 64), idk = (uint32_t)__shfl((int)ident, (int)k, 64);
-        if (!okk) continue;
-        if (idk && ((s ^ d) & 15) == 0) {
-            // same alignment: 16-byte chunks of [d, d+L); partial head/tail chunks by bytes
-            const uint64_t c1 = (d + L + 15) & ~(uint64_t)15;
-            for (uint64_t c = (d & ~(uint64_t)15) + 16u * sub; c < c1; c += 16u * G) {
-                const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + (c - d + s));  // 16-byte aligned too
-                if (c >= d && c + 16 <= d + L && c + 16 <= p.dst_len) {
-                    *reinterpret_cast<uint4*>(p.dst + c) = v;
-                } else {
-                    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                    for (int q = 0; q < 16; q++)
-                        if (c + q >= d && c + q < d + L) put_byte(p, c + q, w[q >> 2] >> (8 * (q & 3)));
-                }
-            }
-        } else if (idk) {
-            // different alignment: destination dwords, source bytes shifted into place
-            const uint64_t w1 = (d + L + 3) & ~(uint64_t)3;
-            for (uint64_t a = (d & ~(uint64_t)3) + 4u * sub; a < w1; a += 4u * G) {
-                const uint64_t sa = a - d + s;  // source of this dword's first byte (may be < s)
-                const uint32_t v = __builtin_amdgcn_alignbyte(slab_dw(p.b, sa + 4), slab_dw(p.b, sa), (uint32_t)(sa & 3));
-                if (a >= d && a + 4 <= d + L && a + 4 <= p.dst_len) {
-                    *reinterpret_cast<uint32_t*>(p.dst + a) = v;
-                } else {
-#pragma unroll
-                    for (int q = 0; q < 4; q++)
-                        if (a + q >= d && a + q < d + L) put_byte(p, a + q, v >> (8 * q));
-                }
-            }
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t t = (uint32_t)__shfl_up((int)incl, (unsigned)m, 64);
+        if (lane >= (uint32_t)m) incl += t;
+    }
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    s_pre[w][lane] = incl - ch;
+    if (lane == 63) s_pre[w][64] = total;
+    s_src[w][lane] = src;
+    s_dst[w][lane] = dst;
+    s_len[w][lane] = len;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    uint32_t k = 0;
+    for (uint32_t g = lane; g < total; g += 64u) {
+        while (s_pre[w][k + 1] <= g) k++;  // packets with no chunks are skipped (pre[64] = total > g)
+        const uint64_t s = s_src[w][k], d = s_dst[w][k];
+        const uint32_t L = s_len[w][k];
+        const uint64_t ca = (d & ~(uint64_t)15) + 16u * (g - s_pre[w][k]);  // destination chunk
+        uint32_t o[4];
+        load_src_chunk(p.b, last16, s, d, ca, o);
+        const uint64_t lo = ca > d ? ca : d, hi = ca + 16 < d + L ? ca + 16 : d + L;
+        if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
+            *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
-            // Q2: output byte q comes from the list entry covering it (header slices, then payload)
-            const uint64_t ik = base + k;
-            uint32_t nh = p.b.n_hdrs[ik];
-            nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
-            for (uint32_t q = sub; q < L; q += G) {
-                uint32_t pos = 0, from = 0xFFFFFFFFu;
-                for (uint32_t j = 0; j < nh; j++) {
-                    const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + ik];
-                    const uint32_t sz = ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
-                    if (from == 0xFFFFFFFFu && q < pos + sz) from = p.b.hdr_off[(uint64_t)j * p.b.n + ik] + (q - pos);
-                    pos += sz;
-                }
-                if (from == 0xFFFFFFFFu) from = p.payload_off[ik] + (q - pos);
-                put_byte(p, d + q, p.b.slab[s + from]);
+            store_edge_chunk(p.dst, p.dst_len, ca, o, lo, hi);
+        }
+    }
+    // ---- Q2 packets (two or more GRE options), one at a time by the whole wave: output byte q
+    // (lane q mod 64) comes from the list entry covering it — header slices, then the payload
+    for (uint64_t q2 = __ballot(ok && !ident); q2; q2 &= q2 - 1) {  // uniform
+        const uint32_t kk = (uint32_t)__builtin_ctzll(q2);
+        const uint64_t ik = base + kk, s = s_src[w][kk], d = s_dst[w][kk];
+        const uint32_t L = s_len[w][kk];
+        uint32_t nh = p.b.n_hdrs[ik];
+        nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
+        for (uint32_t q = lane; q < L; q += 64u) {
+            uint32_t pos = 0, from = 0xFFFFFFFFu;
+            for (uint32_t j = 0; j < nh; j++) {
+                const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + ik];
+                const uint32_t sz = ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
+                if (from == 0xFFFFFFFFu && q < pos + sz) from = p.b.hdr_off[(uint64_t)j * p.b.n + ik] + (q - pos);
+                pos += sz;
             }
+            if (from == 0xFFFFFFFFu) from = p.payload_off[ik] + (q - pos);
+            put_byte(p, d + q, p.b.slab[s + from]);
         }
     }
 }
@@ -294,22 +377,89 @@ struct SParams {
     SSpec s[kMaxSpecs];
 };
 
+// The packet's first kSnch 16-byte chunks (from its 16-byte-aligned start) in LDS at an odd
+// dword stride, as in the parse kernel.
+constexpr int kSnch = 5;
+constexpr uint32_t kSstride = 4 * kSnch + 1;  // dwords
+
+// One setter on a <= 64-bit field whose bytes start at byte x of the lane's LDS window: its <= 9
+// bytes read as one 16-byte big-endian piece, set by one shift and mask, written back to LDS.
+__device__ __forceinline__ void set_in_window(uint32_t* w, uint32_t x, uint32_t lsb, uint32_t msb, uint64_t v) {
+    const uint32_t b0 = lsb >> 3, nb = (msb >> 3) - b0 + 1;
+    const uint32_t k = x >> 2, sh = x & 3;
+    const uint32_t d0 = w[k], d1 = w[k + 1], d2 = w[k + 2], d3 = w[k + 3], d4 = w[k + 4];
+    U128 W{((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(d1, d0, sh)) << 32) |
+               __builtin_bswap32(__builtin_amdgcn_alignbyte(d2, d1, sh)),
+           ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(d3, d2, sh)) << 32) |
+               __builtin_bswap32(__builtin_amdgcn_alignbyte(d4, d3, sh))};
+    put_bits(W, lsb - 8 * b0, msb - 8 * b0, msb - lsb + 1, v, 0);
+    uint8_t* h = reinterpret_cast<uint8_t*>(w) + x;
+    for (uint32_t j = 0; j < nb; j++) h[j] = (uint8_t)((j < 8 ? W.hi >> (56 - 8 * j) : W.lo >> (120 - 8 * j)) & 0xFFu);
+}
+
 __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     __shared__ ChainLds L;
-    const uint32_t t = threadIdx.x;
+    __shared__ uint32_t win[kRwBlock * kSstride + 8];  // +8: the last lane's 16-byte over-read
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave0 = t & ~63u;
     const uint64_t i = (uint64_t)blockIdx.x * kRwBlock + t;
-    if (i >= p.b.n) return;
-    const uint32_t nh = stage_chain(p.b, i, t, L);
-    const uint64_t off = pkt_off(p.b, i);
-    for (uint32_t s = 0; s < p.nspec; s++) {  // specs in order: overlapping ones act as sequential setters
+    const bool act = i < p.b.n;  // no early exit: the wave loads and stores windows together
+    uint32_t nh = 0, plen = 0;
+    uint64_t off = 0;
+    if (act) {
+        nh = stage_chain(p.b, i, t, L);
+        off = pkt_off(p.b, i);
+        plen = p.b.lens ? p.b.lens[i] : p.b.stride;
+        const uint64_t room = off < p.b.slab_len ? p.b.slab_len - off : 0;
+        plen = (uint64_t)plen > room ? (uint32_t)room : plen;
+    }
+    const uint32_t shift = (uint32_t)(off & 15);
+    // window mode iff every field this packet sets is <= 64 bits and lies inside the window
+    bool inwin = act;
+    for (uint32_t s = 0; s < p.nspec && inwin; s++) {
+        const pkt_field_spec_t sp = p.s[s].f;
+        const int32_t ho = act ? find_lds(L, t, nh, sp.hdr_type, sp.occurrence) : -1;
+        if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
+    }
+    // cooperative window loads: in load k, lanes 4j..4j+3 fetch chunks 0-3 of packet 16k + j
+    const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+        const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+        uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
+        a = a > last16 ? last16 : a;
+        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
+        uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+    }
+#pragma unroll
+    for (int c = 4; c < kSnch; c++) {
+        uint64_t a = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
+        a = a > last16 ? last16 : a;
+        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
+        uint32_t* w = win + t * kSstride + 4 * c;
+        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t dirty = 0;  // window chunks holding a set byte
+    for (uint32_t s = 0; s < p.nspec && act; s++) {  // specs in order: overlapping ones act as sequential setters
         const pkt_field_spec_t sp = p.s[s].f;
         const int32_t ho = find_lds(L, t, nh, sp.hdr_type, sp.occurrence);
         if (ho < 0) continue;
         const uint32_t lsb = sp.start, msb = sp.end;
         const uint64_t v0 = p.s[s].values[i];
+        if (inwin) {
+            const uint32_t x = shift + (uint32_t)ho + (lsb >> 3);
+            set_in_window(win + t * kSstride, x, lsb, msb, v0);
+            dirty |= ((2u << ((x + (msb >> 3) - (lsb >> 3)) >> 4)) - 1u) & ~((1u << (x >> 4)) - 1u);
+            continue;
+        }
         if (msb - lsb < 64) {
-            // the field's <= 9 bytes from one 16-byte window read in a single round trip: set by one
-            // shift and mask, then only the field's bytes stored (byte stores: neighbours untouched)
+            // outside the window: the same RMW on one 16-byte read of global memory, only the
+            // field's bytes stored (byte stores: neighbours untouched)
             const uint32_t b0 = lsb >> 3, nb = (msb >> 3) - b0 + 1;
             const uint64_t A = off + (uint32_t)ho + b0;
             const uint32_t sh = (uint32_t)(A & 3);
@@ -321,7 +471,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
                        __builtin_bswap32(__builtin_amdgcn_alignbyte(d4, d3, sh))};
             put_bits(W, lsb - 8 * b0, msb - 8 * b0, msb - lsb + 1, v0, 0);
             uint8_t* h = p.slab + A;
-            for (uint32_t j = 0; j < nb; j++)  // uniform trip count
+            for (uint32_t j = 0; j < nb; j++)
                 h[j] = (uint8_t)((j < 8 ? W.hi >> (56 - 8 * j) : W.lo >> (120 - 8 * j)) & 0xFFu);
             continue;
         }
@@ -340,6 +490,35 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             h[byte] = (uint8_t)(nbit == 8 ? bits : ((h[byte] & ~m) | bits));
             v = nbit >= 64 ? 0 : (v >> nbit);
             b = lo - 1;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // write back the dirty chunks, the packet's own bytes only: chunks 0-3 cooperatively (lanes
+    // 4j..4j+3 store packet 16k + j's 64 bytes), chunk 4 per lane
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+        const uint32_t dr = (uint32_t)__shfl((int)dirty, (int)r, 64);
+        const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+        const uint32_t plr = (uint32_t)__shfl((int)plen, (int)r, 64);
+        if ((dr >> c) & 1u) {
+            const uint64_t ca = (offr & ~(uint64_t)15) + 16u * c;
+            const uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
+            const uint32_t o[4] = {w[0], w[1], w[2], w[3]};
+            store_chunk(p.slab, p.b.slab_len, ca, o, ca > offr ? ca : offr,
+                        ca + 16 < offr + plr ? ca + 16 : offr + plr);
+        }
+    }
+#pragma unroll
+    for (int c = 4; c < kSnch; c++) {
+        if ((dirty >> c) & 1u) {
+            const uint64_t ca = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
+            const uint32_t* w = win + t * kSstride + 4 * c;
+            const uint32_t o[4] = {w[0], w[1], w[2], w[3]};
+            store_chunk(p.slab, p.b.slab_len, ca, o, ca > off ? ca : off, ca + 16 < off + plen ? ca + 16 : off + plen);
         }
     }
 }
