@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <vector>
 
 #include "pktgpu_ctx.hpp"
 #include "pktgpu_device.hpp"
@@ -62,29 +63,36 @@ __device__ __forceinline__ uint32_t slab_dw(const BatchRef& b, uint64_t a) {
     return *reinterpret_cast<const uint32_t*>(b.slab + d);
 }
 
-// The lane's chain in LDS (slot-major [slot][lane]: per-lane byte / u16 reads of one slot are
-// consecutive addresses, conflict-free).  Returns n_hdrs.
+// The lane's chain: its first kChainLds slots in LDS (slot-major [slot][lane]: per-lane byte /
+// u16 reads of one slot are consecutive addresses, conflict-free), deeper slots read from the
+// chain columns in global memory when a search gets there (chains of > 8 headers are rare, and
+// the smaller LDS footprint buys occupancy).
+constexpr uint32_t kChainLds = 8;
 struct ChainLds {
-    uint8_t type[PKT_MAX_HDRS][kRwBlock];
-    uint16_t off[PKT_MAX_HDRS][kRwBlock];
+    uint8_t type[kChainLds][kRwBlock];
+    uint16_t off[kChainLds][kRwBlock];
 };
 
+// Stages packet i's first slots; returns n_hdrs (clamped to PKT_MAX_HDRS).
 __device__ __forceinline__ uint32_t stage_chain(const BatchRef& b, uint64_t i, uint32_t t, ChainLds& L) {
     uint32_t nh = b.n_hdrs[i];
     nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
-    for (uint32_t j = 0; j < nh; j++) {
+    for (uint32_t j = 0; j < nh && j < kChainLds; j++) {
         L.type[j][t] = b.hdr_type[(uint64_t)j * b.n + i];
         L.off[j][t] = b.hdr_off[(uint64_t)j * b.n + i];
     }
     return nh;
 }
 
-// offset of the occurrence-th header of `type` in the lane's chain, or -1
-__device__ __forceinline__ int32_t find_lds(const ChainLds& L, uint32_t t, uint32_t nh, uint32_t type, uint32_t occ) {
+// offset of the occurrence-th header of `type` in packet i's chain, or -1
+__device__ __forceinline__ int32_t find_lds(const ChainLds& L, const BatchRef& b, uint64_t i, uint32_t t, uint32_t nh,
+                                            uint32_t type, uint32_t occ) {
     uint32_t c = 0;
     for (uint32_t j = 0; j < nh; j++) {
-        if (L.type[j][t] == type) {
-            if (c == occ) return (int32_t)L.off[j][t];
+        const bool in = j < kChainLds;
+        const uint32_t ty = in ? L.type[j][t] : b.hdr_type[(uint64_t)j * b.n + i];
+        if (ty == type) {
+            if (c == occ) return (int32_t)(in ? L.off[j][t] : b.hdr_off[(uint64_t)j * b.n + i]);
             c++;
         }
     }
@@ -104,29 +112,49 @@ struct XParams {
 
 // Window of a lane's packet: its first kXnch aligned 16-byte chunks, in LDS at an odd dword stride
 // (per-lane dword reads conflict-free); bytes past it come from global memory (PacketView).
-constexpr int kXnch = 5;
+constexpr int kXnch = 5;  // (>= 4: chunks 0-3 are loaded cooperatively)
 constexpr uint32_t kXstride = 4 * kXnch + 1;  // dwords
 
 __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     __shared__ ChainLds L;
     __shared__ uint32_t win[kRwBlock * kXstride];
-    const uint32_t t = threadIdx.x;
+    const uint32_t t = threadIdx.x, lane = t & 63u, wave0 = t & ~63u;
     const uint64_t i = (uint64_t)blockIdx.x * kRwBlock + t;
-    if (i >= p.b.n) return;  // no barrier below: a lane reads only its own LDS
-    const uint32_t nh = stage_chain(p.b, i, t, L);
-    const uint64_t off = pkt_off(p.b, i);
+    const bool act = i < p.b.n;  // no early exit: the wave loads its windows together
+    const uint64_t off = act ? pkt_off(p.b, i) : 0u;
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
     uint32_t* w = win + t * kXstride;
+    // cooperative window loads, issued before the chain is staged so that both are in flight
+    // together: in load k, lanes 4j..4j+3 fetch chunks 0-3 of packet 16k + j (64 contiguous bytes
+    // per 4 lanes, as in the parse kernel); chunk 4 per lane
+    uint4 v[kXnch];
 #pragma unroll
-    for (int c = 0; c < kXnch; c++) {
+    for (uint32_t k = 0; k < 4; k++) {
+        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+        const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+        uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
+        a = a > last16 ? last16 : a;
+        v[k] = *reinterpret_cast<const uint4*>(p.b.slab + a);
+    }
+#pragma unroll
+    for (int c = 4; c < kXnch; c++) {
         uint64_t o = (off & ~(uint64_t)15) + 16u * c;
         o = o > last16 ? last16 : o;
-        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + o);
-        w[4 * c] = v.x;
-        w[4 * c + 1] = v.y;
-        w[4 * c + 2] = v.z;
-        w[4 * c + 3] = v.w;
+        v[c] = *reinterpret_cast<const uint4*>(p.b.slab + o);
     }
+    const uint32_t nh = act ? stage_chain(p.b, i, t, L) : 0u;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; k++) {
+        uint32_t* wr = win + (wave0 + 16u * k + (lane >> 2)) * kXstride + 4 * (lane & 3u);
+        wr[0] = v[k].x, wr[1] = v[k].y, wr[2] = v[k].z, wr[3] = v[k].w;
+    }
+#pragma unroll
+    for (int c = 4; c < kXnch; c++) w[4 * c] = v[c].x, w[4 * c + 1] = v[c].y, w[4 * c + 2] = v[c].z, w[4 * c + 3] = v[c].w;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (!act) return;
     PacketView pv;
     pv.lw = reinterpret_cast<const uint8_t*>(w);
     pv.slab = p.b.slab;
@@ -136,10 +164,15 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     pv.win_lo = 0;
     pv.win_end = 16u * kXnch - pv.shift;
     pv.len = 0xFFFFFFFFu;  // (le() does not use it)
-    __builtin_amdgcn_wave_barrier();
+    uint32_t last_ty = 0xFFFFFFFFu, last_occ = 0;
+    int32_t ho = -1;
     for (uint32_t s = 0; s < p.nspec; s++) {  // uniform
         const pkt_field_spec_t sp = p.s[s].f;
-        const int32_t ho = find_lds(L, t, nh, sp.hdr_type, sp.occurrence);
+        if (sp.hdr_type != last_ty || sp.occurrence != last_occ) {  // consecutive specs of one header: one search
+            ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
+            last_ty = sp.hdr_type;
+            last_occ = sp.occurrence;
+        }
         uint64_t v = 0;
         if (ho >= 0) {
             const uint32_t start = sp.start, end = sp.end, wd = end - start + 1;
@@ -417,7 +450,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     bool inwin = act;
     for (uint32_t s = 0; s < p.nspec && inwin; s++) {
         const pkt_field_spec_t sp = p.s[s].f;
-        const int32_t ho = act ? find_lds(L, t, nh, sp.hdr_type, sp.occurrence) : -1;
+        const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
         if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
     }
     // cooperative window loads: in load k, lanes 4j..4j+3 fetch chunks 0-3 of packet 16k + j
@@ -447,7 +480,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     uint32_t dirty = 0;  // window chunks holding a set byte
     for (uint32_t s = 0; s < p.nspec && act; s++) {  // specs in order: overlapping ones act as sequential setters
         const pkt_field_spec_t sp = p.s[s].f;
-        const int32_t ho = find_lds(L, t, nh, sp.hdr_type, sp.occurrence);
+        const int32_t ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
         if (ho < 0) continue;
         const uint32_t lsb = sp.start, msb = sp.end;
         const uint64_t v0 = p.s[s].values[i];
@@ -529,7 +562,7 @@ __global__ __launch_bounds__(kRwBlock) void ipv4_update_kernel(BatchRef b, uint8
     const uint64_t i = (uint64_t)blockIdx.x * kRwBlock + t;
     if (i >= b.n) return;
     const uint32_t nh = stage_chain(b, i, t, L);
-    const int32_t ho = find_lds(L, t, nh, PKT_HDR_IPV4, occurrence);
+    const int32_t ho = find_lds(L, b, i, t, nh, PKT_HDR_IPV4, occurrence);
     if (ho < 0) return;
     const uint64_t a = pkt_off(b, i) + (uint32_t)ho;
     const uint32_t sh = (uint32_t)(a & 3);
@@ -623,12 +656,26 @@ int pkt_extract_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* 
         if (bad_spec(specs[s]) || !values[s]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad field spec");
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    // specs grouped by (header, occurrence), so that the kernel searches the chain once per group;
+    // the order is kept when two specs share an output array (the later one must win)
+    std::vector<uint32_t> ord(nspec);
+    for (uint32_t s = 0; s < nspec; s++) ord[s] = s;
+    bool shared = false;
+    for (uint32_t a = 0; a < nspec && !shared; a++)
+        for (uint32_t c = a + 1; c < nspec && !shared; c++)
+            shared = values[a] == values[c] || (found && found[a] && found[a] == found[c]);
+    if (!shared)
+        std::stable_sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) {
+            return specs[x].hdr_type != specs[y].hdr_type ? specs[x].hdr_type < specs[y].hdr_type
+                                                          : specs[x].occurrence < specs[y].occurrence;
+        });
     for (uint32_t s0 = 0; s0 < nspec; s0 += kMaxSpecs) {  // one launch per 32 specs
         xp.nspec = std::min<uint32_t>(kMaxSpecs, nspec - s0);
         for (uint32_t k = 0; k < xp.nspec; k++) {
-            xp.s[k].f = specs[s0 + k];
-            xp.s[k].values = values[s0 + k];
-            xp.s[k].found = found ? found[s0 + k] : nullptr;
+            const uint32_t q = ord[s0 + k];
+            xp.s[k].f = specs[q];
+            xp.s[k].values = values[q];
+            xp.s[k].found = found ? found[q] : nullptr;
         }
         hipLaunchKernelGGL(extract_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), xp);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "extract_kernel launch");

@@ -201,7 +201,9 @@ def test_empty_batch(P):
     del pktgpu
 
 
-def test_depth_limit_and_stacks(P):
+def _stack_packets():
+    """VLAN stacks of 0-19 tags (whole and truncated) and MPLS stacks of 1-18 labels, at a 256-B
+    stride with lengths: chains past the depth limit and far past 8 headers."""
     eth = gen.ethernet("00:00:00:00:00:01", "00:00:00:00:00:02", 0x8100).data
     tag = gen.vlan(1, 0, 7, 0x8100).data
     last = gen.vlan(0, 0, 5, 0x0800).data
@@ -222,7 +224,12 @@ def test_depth_limit_and_stacks(P):
     for i, p in enumerate(pkts):
         slab[i, :len(p)] = np.frombuffer(p, np.uint8)
         lens[i] = len(p)
-    g, o = both(P, slab, len(pkts), stride=stride, lens=lens, label="stacks")
+    return slab, lens, stride
+
+
+def test_depth_limit_and_stacks(P):
+    slab, lens, stride = _stack_packets()
+    g, o = both(P, slab, len(lens), stride=stride, lens=lens, label="stacks")
     assert (g["status"] == schema.DEPTH_LIMIT).sum() > 5 and (g["status"] == 0).sum() > 5
 
 
@@ -300,6 +307,33 @@ def test_extract_fields_vs_oracle(P):
         assert np.array_equal(vals[k].cpu().numpy(), ov[k]), sp
         assert np.array_equal(found[k].cpu().numpy(), of[k]), sp
     del pc, offs, lens
+
+
+def test_extract_and_set_fields_deep_chains(P):
+    """Getters and setters on headers deep in the chain (slot >= 8: the kernels keep the first 8
+    slots in LDS and read deeper ones from the chain columns), vs the oracle."""
+    slab, lens, stride = _stack_packets()
+    n = len(lens)
+    g = gpu_parse(P, slab, n, stride=stride, lens=lens, columns=["chain"])
+    ch = {k: g[k] for k in ("n_hdrs", "hdr_type", "hdr_off")}
+    specs = [(H["Vlan"], k, 4, 15) for k in range(0, 16, 3)] + [(H["MPLS"], k, 0, 19) for k in range(0, 16, 5)]
+    specs += [(H["IPv4"], 0, 96, 127), (H["UDP"], 0, 0, 15), (H["Ether"], 0, 96, 111)]
+    vals, found = P.extract_fields(dev(slab), {k: dev(v) for k, v in ch.items()}, specs, stride=stride,
+                                   lens=dev(lens))
+    torch.cuda.synchronize()
+    ov, of = oracle.extract_fields(slab, n, ch, specs, stride=stride, lens=lens)
+    for k, sp in enumerate(specs):
+        assert np.array_equal(vals[k].cpu().numpy(), ov[k]), sp
+        assert np.array_equal(found[k].cpu().numpy(), of[k]), sp
+    rng = np.random.default_rng(11)
+    sv = [rng.integers(0, 2**63, n, dtype=np.uint64) for _ in specs]
+    ds = dev(slab.reshape(-1).copy())
+    P.set_fields(ds, {k: dev(v) for k, v in ch.items()}, specs, [dev(v) for v in sv], n=n, stride=stride,
+                 lens=dev(lens))
+    torch.cuda.synchronize()
+    want = slab.reshape(-1).copy()
+    oracle.set_fields(want, n, ch, specs, sv, stride=stride, lens=lens)
+    assert np.array_equal(ds.cpu().numpy(), want)
 
 
 def test_ipv4_checksum_batch_sweep(P):
