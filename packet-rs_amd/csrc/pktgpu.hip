@@ -254,6 +254,9 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
 #ifndef PKTGPU_WAVES_PER_EU
 #define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
 #endif
+#ifndef PKTGPU_COOP_ALL
+#define PKTGPU_COOP_ALL 1  // every window chunk cooperative (0: chunks 0-3 cooperative, 4.. per lane)
+#endif
 #ifndef PKTGPU_COOP_FIXED
 #define PKTGPU_COOP_FIXED 1  // fixed-stride batches load their windows cooperatively too
 #endif
@@ -281,6 +284,27 @@ void parse_kernel(KParams p) {
         if (act) packet_range(p, base + threadIdx.x, off, len);
         const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
         const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+#if PKTGPU_COOP_ALL
+        // All NCH chunks of the wave's 64 windows as 64*NCH (record, chunk) pairs, pair 64k + lane
+        // in load k: consecutive lanes fetch consecutive chunks of one record, so each window's
+        // bytes come from one or two wave instructions instead of a cooperative 64-byte piece plus
+        // per-lane chunks (separate instructions to the same 128-B line re-request it from memory:
+        // scripts/fetch_calib.py).
+#pragma unroll
+        for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+            const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
+            const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                                  (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+            uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
+            a = a > last16 ? last16 : a;
+            const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
+            uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
+        }
+#else
 #pragma unroll
         for (uint32_t k = 0; k < 4; k++) {
             const uint32_t r = 16u * k + (wl >> 2), c = wl & 3u;
@@ -306,6 +330,7 @@ void parse_kernel(KParams p) {
             w[2] = v.z;
             w[3] = v.w;
         }
+#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");

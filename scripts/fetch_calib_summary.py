@@ -3,12 +3,13 @@
 FETCH_SIZE bytes per item next to the bytes, 64-B sectors and 128-B lines each item touches."""
 import collections
 import csv
+import glob
 import json
 import sys
 
 d, planf = sys.argv[1], sys.argv[2]
 meta = json.load(open(planf))
-rows = [r for r in csv.DictReader(open(f"{d}/pmc_counter_collection.csv")) if "fetch_kernel" in r["Kernel_Name"]]
+rows = [r for r in csv.DictReader(open(glob.glob(f"{d}/**/*counter_collection.csv", recursive=True)[0])) if "fetch_kernel" in r["Kernel_Name"]]
 by = collections.OrderedDict()
 for r in rows:
     by.setdefault(int(r["Dispatch_Id"]), 0.0)
