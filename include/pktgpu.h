@@ -328,6 +328,14 @@ int pkt_set_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *
                    const pkt_field_spec_t *specs, uint32_t nspec, const uint64_t *const *values,
                    void *stream);
 
+/* pkt_set_fields followed, in the same launch, by pkt_ipv4_update_checksum of the
+ * `ipv4_occurrence`-th IPv4 header (< 0: no checksum refresh; nspec may then be 0 for a refresh
+ * alone): the header rewrite of the update+clone loop (tests/lib.rs:778-787: setters, then
+ * utils.rs:233-236's checksum) as one pass over each packet's bytes. */
+int pkt_set_fields_csum(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
+                        const pkt_field_spec_t *specs, uint32_t nspec, const uint64_t *const *values,
+                        int32_t ipv4_occurrence, void *stream);
+
 /* `ipv4.set_header_checksum(Packet::ipv4_checksum(ipv4.to_vec()))` (utils.rs:233-236;
  * packet.rs:93-107 with the Q1 fold) on the `occurrence`-th IPv4 header of every packet, in
  * place.  Packets without that header are untouched. */

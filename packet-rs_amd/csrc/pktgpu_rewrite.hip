@@ -112,7 +112,7 @@ struct XParams {
 
 // Window of a lane's packet: its first kXnch aligned 16-byte chunks, in LDS at an odd dword stride
 // (per-lane dword reads conflict-free); bytes past it come from global memory (PacketView).
-constexpr int kXnch = 5;  // (>= 4: chunks 0-3 are loaded cooperatively)
+constexpr int kXnch = 5;
 constexpr uint32_t kXstride = 4 * kXnch + 1;  // dwords
 
 __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
@@ -125,32 +125,25 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
     uint32_t* w = win + t * kXstride;
     // cooperative window loads, issued before the chain is staged so that both are in flight
-    // together: in load k, lanes 4j..4j+3 fetch chunks 0-3 of packet 16k + j (64 contiguous bytes
-    // per 4 lanes, as in the parse kernel); chunk 4 per lane
+    // together: the wave's 64 windows as 64*kXnch (packet, chunk) pairs, pair 64k + lane in load k
+    // (consecutive lanes, consecutive chunks of one packet, as in the parse kernel)
     uint4 v[kXnch];
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+    for (uint32_t k = 0; k < (uint32_t)kXnch; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kXnch, c = pid % (uint32_t)kXnch;
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
         uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
         a = a > last16 ? last16 : a;
         v[k] = *reinterpret_cast<const uint4*>(p.b.slab + a);
     }
-#pragma unroll
-    for (int c = 4; c < kXnch; c++) {
-        uint64_t o = (off & ~(uint64_t)15) + 16u * c;
-        o = o > last16 ? last16 : o;
-        v[c] = *reinterpret_cast<const uint4*>(p.b.slab + o);
-    }
     const uint32_t nh = act ? stage_chain(p.b, i, t, L) : 0u;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        uint32_t* wr = win + (wave0 + 16u * k + (lane >> 2)) * kXstride + 4 * (lane & 3u);
+    for (uint32_t k = 0; k < (uint32_t)kXnch; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kXnch, c = pid % (uint32_t)kXnch;
+        uint32_t* wr = win + (wave0 + r) * kXstride + 4 * c;
         wr[0] = v[k].x, wr[1] = v[k].y, wr[2] = v[k].z, wr[3] = v[k].w;
     }
-#pragma unroll
-    for (int c = 4; c < kXnch; c++) w[4 * c] = v[c].x, w[4 * c + 1] = v[c].y, w[4 * c + 2] = v[c].z, w[4 * c + 3] = v[c].w;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -407,6 +400,7 @@ struct SParams {
     BatchRef b;
     uint8_t* slab;
     uint32_t nspec;
+    int32_t csum_occ;  // >= 0: refresh that IPv4 header's checksum after the setters
     SSpec s[kMaxSpecs];
 };
 
@@ -453,25 +447,19 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
         const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
         if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
     }
-    // cooperative window loads: in load k, lanes 4j..4j+3 fetch chunks 0-3 of packet 16k + j
+    // cooperative window loads: the wave's 64 windows as 64*kSnch (packet, chunk) pairs, pair
+    // 64k + lane in load k (consecutive lanes, consecutive chunks of one packet: each window from
+    // one or two wave instructions, as in the parse kernel)
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
         uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
         a = a > last16 ? last16 : a;
         const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
         uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
-    }
-#pragma unroll
-    for (int c = 4; c < kSnch; c++) {
-        uint64_t a = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
-        a = a > last16 ? last16 : a;
-        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
-        uint32_t* w = win + t * kSstride + 4 * c;
         w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -525,14 +513,49 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             b = lo - 1;
         }
     }
+    // Packet::ipv4_checksum refresh of the csum_occ-th IPv4 header (ipv4_update_kernel's sum) after
+    // the setters: header dwords inside the window from LDS, past it from global memory (bytes only
+    // this lane wrote); the two checksum bytes into LDS (dirty) or global memory likewise.
+    if (p.csum_occ >= 0 && act) {
+        const int32_t ho = find_lds(L, p.b, i, t, nh, PKT_HDR_IPV4, (uint32_t)p.csum_occ);
+        if (ho >= 0) {
+            const uint32_t x = shift + (uint32_t)ho, x0 = x & ~3u, sh = x & 3u;
+            const uint64_t a0 = off & ~(uint64_t)15;  // window byte q <-> slab byte a0 + q
+            const uint32_t* w = win + t * kSstride;
+            uint32_t d[6];
+#pragma unroll
+            for (int k = 0; k < 6; k++) {
+                const uint32_t q = x0 + 4u * k;
+                d[k] = (inwin && q + 4 <= 16u * kSnch) ? w[q >> 2] : slab_dw(p.b, a0 + q);
+            }
+            uint32_t sum = 0;
+#pragma unroll
+            for (int k = 0; k < 5; k++) {
+                const uint32_t v = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh));
+                sum += (v >> 16) + (k == 2 ? 0u : (v & 0xFFFFu));  // bytes 10-11 (the checksum) skipped
+            }
+            sum = ((sum >> 16) + sum) & 0xFFFFu;  // packet.rs:102-104 (Q1)
+            const uint32_t c = (~sum) & 0xFFFFu;
+#pragma unroll
+            for (uint32_t j = 0; j < 2; j++) {
+                const uint32_t q = x + 10u + j;
+                const uint8_t byte = (uint8_t)(j ? c : c >> 8);
+                if (inwin && q < 16u * kSnch) {
+                    reinterpret_cast<uint8_t*>(win + t * kSstride)[q] = byte;
+                    dirty |= 1u << (q >> 4);
+                } else {
+                    p.slab[a0 + q] = byte;
+                }
+            }
+        }
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // write back the dirty chunks, the packet's own bytes only: chunks 0-3 cooperatively (lanes
-    // 4j..4j+3 store packet 16k + j's 64 bytes), chunk 4 per lane
+    // write back the dirty chunks, the packet's own bytes only, with the pairs of the loads
 #pragma unroll
-    for (uint32_t k = 0; k < 4; k++) {
-        const uint32_t r = 16u * k + (lane >> 2), c = lane & 3u;
+    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
         const uint32_t dr = (uint32_t)__shfl((int)dirty, (int)r, 64);
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
@@ -543,15 +566,6 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             const uint32_t o[4] = {w[0], w[1], w[2], w[3]};
             store_chunk(p.slab, p.b.slab_len, ca, o, ca > offr ? ca : offr,
                         ca + 16 < offr + plr ? ca + 16 : offr + plr);
-        }
-    }
-#pragma unroll
-    for (int c = 4; c < kSnch; c++) {
-        if ((dirty >> c) & 1u) {
-            const uint64_t ca = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
-            const uint32_t* w = win + t * kSstride + 4 * c;
-            const uint32_t o[4] = {w[0], w[1], w[2], w[3]};
-            store_chunk(p.slab, p.b.slab_len, ca, o, ca > off ? ca : off, ca + 16 < off + plen ? ca + 16 : off + plen);
         }
     }
 }
@@ -708,11 +722,11 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
     return PKT_SUCCESS;
 }
 
-int pkt_set_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
-                   const pkt_field_spec_t* specs, uint32_t nspec, const uint64_t* const* values,
-                   void* stream) {
+int pkt_set_fields_csum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
+                        const pkt_field_spec_t* specs, uint32_t nspec, const uint64_t* const* values,
+                        int32_t ipv4_occurrence, void* stream) {
     if (!ctx || !b || (nspec && (!specs || !values))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (b->n == 0 || nspec == 0) return PKT_SUCCESS;
+    if (b->n == 0 || (nspec == 0 && ipv4_occurrence < 0)) return PKT_SUCCESS;
     SParams sp;
     int rc = batch_ref(ctx, b, chain, sp.b);
     if (rc) return rc;
@@ -721,17 +735,28 @@ int pkt_set_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chai
         if (bad_spec(specs[s]) || !values[s]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad field spec");
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    // one thread per packet applies its specs in order; more than 32 specs: ordered launches
-    for (uint32_t s0 = 0; s0 < nspec; s0 += kMaxSpecs) {
+    // one thread per packet applies its specs in order; more than 32 specs: ordered launches, the
+    // checksum refresh in the last one
+    uint32_t s0 = 0;
+    do {
         sp.nspec = std::min<uint32_t>(kMaxSpecs, nspec - s0);
+        sp.csum_occ = s0 + sp.nspec >= nspec ? ipv4_occurrence : -1;
         for (uint32_t k = 0; k < sp.nspec; k++) {
             sp.s[k].f = specs[s0 + k];
             sp.s[k].values = values[s0 + k];
         }
         hipLaunchKernelGGL(set_fields_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), sp);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "set_fields_kernel launch");
-    }
+        s0 += sp.nspec;
+    } while (s0 < nspec);
     return PKT_SUCCESS;
+}
+
+int pkt_set_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,
+                   const pkt_field_spec_t* specs, uint32_t nspec, const uint64_t* const* values,
+                   void* stream) {
+    if (ctx && b && nspec == 0) return PKT_SUCCESS;
+    return pkt_set_fields_csum(ctx, b, chain, specs, nspec, values, -1, stream);
 }
 
 int pkt_ipv4_update_checksum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain,

@@ -267,9 +267,10 @@ class Parser:
         return ch
 
     def set_fields(self, slab, chain, specs, values, stride=None, n=None, offsets=None, lens=None,
-                   stream=None):
+                   stream=None, ipv4_checksum=None):
         """In-place batched `<Hdr>::set_<field>(v)`: specs = [(hdr_type|name, occurrence, start,
-        end)], values = one uint64 device tensor per spec."""
+        end)], values = one uint64 device tensor per spec.  ipv4_checksum=occ also refreshes that
+        IPv4 header's checksum after the setters, in the same launch (pkt_set_fields_csum)."""
         b = self._batch(slab, n, stride, offsets, lens)
         k = len(specs)
         sp = (self._lib.PktFieldSpec * max(1, k))()
@@ -277,8 +278,13 @@ class Parser:
             t = HDR_ID[t] if isinstance(t, str) else int(t)
             sp[i] = self._lib.PktFieldSpec(t, occ, s, e, 0)
         vp = (ctypes.c_void_p * max(1, k))(*[v.data_ptr() for v in values])
-        self._check(self._L.pkt_set_fields(self._ctx, ctypes.byref(b), ctypes.byref(self._chain(chain)),
-                                           sp, k, vp, self._stream(stream)), "pkt_set_fields")
+        if ipv4_checksum is None:
+            self._check(self._L.pkt_set_fields(self._ctx, ctypes.byref(b), ctypes.byref(self._chain(chain)),
+                                               sp, k, vp, self._stream(stream)), "pkt_set_fields")
+        else:
+            self._check(self._L.pkt_set_fields_csum(self._ctx, ctypes.byref(b), ctypes.byref(self._chain(chain)),
+                                                    sp, k, vp, int(ipv4_checksum), self._stream(stream)),
+                        "pkt_set_fields_csum")
 
     def ipv4_update_checksum(self, slab, chain, occurrence=0, stride=None, n=None, offsets=None,
                              lens=None, stream=None):

@@ -77,6 +77,9 @@ SIGNATURES = {
     "pkt_set_fields": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
                                       ctypes.POINTER(PktFieldSpec), ctypes.c_uint32,
                                       ctypes.POINTER(_P), _P]),
+    "pkt_set_fields_csum": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
+                                           ctypes.POINTER(PktFieldSpec), ctypes.c_uint32,
+                                           ctypes.POINTER(_P), ctypes.c_int32, _P]),
     "pkt_ipv4_update_checksum": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),
                                                 ctypes.c_uint32, _P]),
     "pkt_broadcast": (ctypes.c_int, [_P, _P, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, _P, _P]),

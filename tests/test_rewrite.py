@@ -70,8 +70,13 @@ def test_gpu_set_fields_and_checksum_vs_oracle():
     import pktgpu
     P = pktgpu.Parser(0)
     rng = np.random.default_rng(7)
-    for kind in ("c3", "c4"):
-        if kind == "c3":
+    for kind in ("c2", "c3", "c4"):
+        if kind == "c2":
+            n = 40000
+            slab = gen.gen_c2(n, seed=6).reshape(-1).copy()
+            kw = dict(stride=64)
+            dkw = dict(stride=64)
+        elif kind == "c3":
             n = 40000
             slab = gen.gen_c3(n, seed=8).reshape(-1).copy()
             kw = dict(stride=128)
@@ -84,6 +89,7 @@ def test_gpu_set_fields_and_checksum_vs_oracle():
             dkw = dict(offsets=torch.from_numpy(offs).cuda(), lens=torch.from_numpy(lens).cuda())
         ch = oracle.parse_batch(slab, n, columns=["n_hdrs", "hdr_type", "hdr_off"], **kw)
         specs, vals = _specs_and_values(n, rng)
+        slab0 = slab.copy()
         ds = torch.from_numpy(slab.copy()).cuda()
         dch = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in ch.items()}
         P.set_fields(ds, dch, specs, [torch.from_numpy(v).cuda() for v in vals], n=n, **dkw)
@@ -95,3 +101,10 @@ def test_gpu_set_fields_and_checksum_vs_oracle():
         oracle.ipv4_update_checksum(slab, n, ch, 1, **kw)
         got = ds.cpu().numpy()
         assert np.array_equal(got, slab), kind
+        # the fused form (setters + one checksum refresh in one launch) on the same inputs
+        ds2 = torch.from_numpy(slab0).cuda()
+        for occ in (0, 1):
+            P.set_fields(ds2, dch, specs if occ == 0 else [], [torch.from_numpy(v).cuda() for v in vals] if occ == 0 else [],
+                         n=n, ipv4_checksum=occ, **dkw)
+        torch.cuda.synchronize()
+        assert np.array_equal(ds2.cpu().numpy(), slab), kind + " fused"
