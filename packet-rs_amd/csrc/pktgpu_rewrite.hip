@@ -73,15 +73,41 @@ struct ChainLds {
     uint16_t off[kChainLds][kRwBlock];
 };
 
-// Stages packet i's first slots; returns n_hdrs (clamped to PKT_MAX_HDRS).
-__device__ __forceinline__ uint32_t stage_chain(const BatchRef& b, uint64_t i, uint32_t t, ChainLds& L) {
-    uint32_t nh = b.n_hdrs[i];
-    nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
-    for (uint32_t j = 0; j < nh && j < kChainLds; j++) {
+// Stage packet i's first slots in LDS: chain_load issues n_hdrs and the first 4 slot rows
+// unconditionally (the columns are [PKT_MAX_HDRS][n], so rows past n_hdrs are readable; their
+// bytes are never used), so that they are in flight together with the caller's other loads: one
+// memory round trip for the common chains instead of one per slot.  chain_store writes them and
+// loads any deeper slots; returns n_hdrs (clamped to PKT_MAX_HDRS).
+static_assert(PKT_MAX_HDRS >= 4 && kChainLds >= 4, "first 4 slot rows staged unconditionally");
+struct ChainPre {
+    uint32_t nh, ty[4], of[4];
+};
+__device__ __forceinline__ ChainPre chain_load(const BatchRef& b, uint64_t i) {
+    ChainPre c;
+    c.nh = b.n_hdrs[i];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        c.ty[j] = b.hdr_type[(uint64_t)j * b.n + i];
+        c.of[j] = b.hdr_off[(uint64_t)j * b.n + i];
+    }
+    return c;
+}
+__device__ __forceinline__ uint32_t chain_store(const BatchRef& b, uint64_t i, uint32_t t, ChainLds& L, const ChainPre& c) {
+    const uint32_t nh = c.nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : c.nh;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        L.type[j][t] = (uint8_t)c.ty[j];
+        L.off[j][t] = (uint16_t)c.of[j];
+    }
+    for (uint32_t j = 4; j < nh && j < kChainLds; j++) {
         L.type[j][t] = b.hdr_type[(uint64_t)j * b.n + i];
         L.off[j][t] = b.hdr_off[(uint64_t)j * b.n + i];
     }
     return nh;
+}
+
+__device__ __forceinline__ uint32_t stage_chain(const BatchRef& b, uint64_t i, uint32_t t, ChainLds& L) {
+    return chain_store(b, i, t, L, chain_load(b, i));
 }
 
 // offset of the occurrence-th header of `type` in packet i's chain, or -1
@@ -118,6 +144,9 @@ constexpr uint32_t kXstride = 4 * kXnch + 1;  // dwords
 __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     __shared__ ChainLds L;
     __shared__ uint32_t win[kRwBlock * kXstride];
+    // The spec table in LDS: indexed by the loop counter, the kernel-argument copy is read with a
+    // vector load and a full memory round trip per spec; from LDS it is one broadcast read.
+    __shared__ XSpec S[kMaxSpecs];
     const uint32_t t = threadIdx.x, lane = t & 63u, wave0 = t & ~63u;
     const uint64_t i = (uint64_t)blockIdx.x * kRwBlock + t;
     const bool act = i < p.b.n;  // no early exit: the wave loads its windows together
@@ -137,16 +166,20 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
         a = a > last16 ? last16 : a;
         v[k] = *reinterpret_cast<const uint4*>(p.b.slab + a);
     }
-    const uint32_t nh = act ? stage_chain(p.b, i, t, L) : 0u;
+    ChainPre cp{};
+    if (act) cp = chain_load(p.b, i);
+    XSpec xs{};
+    if (t < p.nspec) xs = p.s[t];
+    // every load above is in flight; now the LDS stores
+    if (t < p.nspec) S[t] = xs;
 #pragma unroll
     for (uint32_t k = 0; k < (uint32_t)kXnch; k++) {
         const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kXnch, c = pid % (uint32_t)kXnch;
         uint32_t* wr = win + (wave0 + r) * kXstride + 4 * c;
         wr[0] = v[k].x, wr[1] = v[k].y, wr[2] = v[k].z, wr[3] = v[k].w;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t nh = act ? chain_store(p.b, i, t, L, cp) : 0u;
+    __syncthreads();  // the spec table (and every wave's windows)
     if (!act) return;
     PacketView pv;
     pv.lw = reinterpret_cast<const uint8_t*>(w);
@@ -160,7 +193,7 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     uint32_t last_ty = 0xFFFFFFFFu, last_occ = 0;
     int32_t ho = -1;
     for (uint32_t s = 0; s < p.nspec; s++) {  // uniform
-        const pkt_field_spec_t sp = p.s[s].f;
+        const pkt_field_spec_t sp = S[s].f;
         if (sp.hdr_type != last_ty || sp.occurrence != last_occ) {  // consecutive specs of one header: one search
             ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
             last_ty = sp.hdr_type;
@@ -188,8 +221,8 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
             if (w2 != 0 && w2 < 64) val &= (1ull << w2) - 1;
             v = val;
         }
-        p.s[s].values[i] = v;
-        if (p.s[s].found) p.s[s].found[i] = ho >= 0 ? 1 : 0;
+        S[s].values[i] = v;
+        if (S[s].found) S[s].found[i] = ho >= 0 ? 1 : 0;
     }
 }
 
@@ -355,6 +388,9 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    // One chunk per lane per round.  (Issuing 4 or 8 rounds' loads before their stores was slower:
+    // C2 45 / 141 vs 33 us, C4 135 / 422 vs 125 us — 120+ VGPRs halve the resident waves,
+    // profiles/ab/r02tv_to_vec_unroll.txt.)
     uint32_t k = 0;
     for (uint32_t g = lane; g < total; g += 64u) {
         while (s_pre[w][k + 1] <= g) k++;  // packets with no chunks are skipped (pre[64] = total > g)
@@ -408,6 +444,7 @@ struct SParams {
 // dword stride, as in the parse kernel.
 constexpr int kSnch = 5;
 constexpr uint32_t kSstride = 4 * kSnch + 1;  // dwords
+constexpr uint32_t kPreVals = 4;  // setter values prefetched into registers
 
 // One setter on a <= 64-bit field whose bytes start at byte x of the lane's LDS window: its <= 9
 // bytes read as one 16-byte big-endian piece, set by one shift and mask, written back to LDS.
@@ -427,30 +464,24 @@ __device__ __forceinline__ void set_in_window(uint32_t* w, uint32_t x, uint32_t 
 __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     __shared__ ChainLds L;
     __shared__ uint32_t win[kRwBlock * kSstride + 8];  // +8: the last lane's 16-byte over-read
+    __shared__ SSpec S[kMaxSpecs];  // the spec table in LDS (as in extract_kernel)
     const uint32_t t = threadIdx.x, lane = t & 63u, wave0 = t & ~63u;
     const uint64_t i = (uint64_t)blockIdx.x * kRwBlock + t;
     const bool act = i < p.b.n;  // no early exit: the wave loads and stores windows together
-    uint32_t nh = 0, plen = 0;
+    uint32_t plen = 0;
     uint64_t off = 0;
     if (act) {
-        nh = stage_chain(p.b, i, t, L);
         off = pkt_off(p.b, i);
         plen = p.b.lens ? p.b.lens[i] : p.b.stride;
         const uint64_t room = off < p.b.slab_len ? p.b.slab_len - off : 0;
         plen = (uint64_t)plen > room ? (uint32_t)room : plen;
     }
-    const uint32_t shift = (uint32_t)(off & 15);
-    // window mode iff every field this packet sets is <= 64 bits and lies inside the window
-    bool inwin = act;
-    for (uint32_t s = 0; s < p.nspec && inwin; s++) {
-        const pkt_field_spec_t sp = p.s[s].f;
-        const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
-        if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
-    }
-    // cooperative window loads: the wave's 64 windows as 64*kSnch (packet, chunk) pairs, pair
-    // 64k + lane in load k (consecutive lanes, consecutive chunks of one packet: each window from
-    // one or two wave instructions, as in the parse kernel)
+    // All loads first, in flight together: the windows (cooperative: the wave's 64 windows as
+    // 64*kSnch (packet, chunk) pairs, pair 64k + lane in load k, so each window comes from one or
+    // two wave instructions, as in the parse kernel), the chain, the first kPreVals values (their
+    // pointers are kernel arguments at constant indices: scalar loads) and the spec table.
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    uint4 v[kSnch];
 #pragma unroll
     for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
         const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
@@ -458,25 +489,44 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
         uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
         a = a > last16 ? last16 : a;
-        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
-        uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
-        w[0] = v.x, w[1] = v.y, w[2] = v.z, w[3] = v.w;
+        v[k] = *reinterpret_cast<const uint4*>(p.b.slab + a);
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    ChainPre cp{};
+    if (act) cp = chain_load(p.b, i);
+    uint64_t vpre[kPreVals];
+#pragma unroll
+    for (uint32_t s = 0; s < kPreVals; s++) vpre[s] = (act && s < p.nspec) ? p.s[s].values[i] : 0u;
+    SSpec ss{};
+    if (t < p.nspec) ss = p.s[t];
+    if (t < p.nspec) S[t] = ss;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
+        uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
+        w[0] = v[k].x, w[1] = v[k].y, w[2] = v[k].z, w[3] = v[k].w;
+    }
+    const uint32_t nh = act ? chain_store(p.b, i, t, L, cp) : 0u;
+    __syncthreads();  // the spec table and the windows
+    const uint32_t shift = (uint32_t)(off & 15);
+    // window mode iff every field this packet sets is <= 64 bits and lies inside the window
+    bool inwin = act;
+    for (uint32_t s = 0; s < p.nspec && inwin; s++) {
+        const pkt_field_spec_t sp = S[s].f;
+        const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
+        if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
+    }
     uint32_t dirty = 0;  // window chunks holding a set byte
-    for (uint32_t s = 0; s < p.nspec && act; s++) {  // specs in order: overlapping ones act as sequential setters
-        const pkt_field_spec_t sp = p.s[s].f;
+    // one setter (specs in order: overlapping ones act as sequential setters)
+    auto apply = [&](uint32_t s, uint64_t v0) {
+        const pkt_field_spec_t sp = S[s].f;
         const int32_t ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
-        if (ho < 0) continue;
+        if (ho < 0) return;
         const uint32_t lsb = sp.start, msb = sp.end;
-        const uint64_t v0 = p.s[s].values[i];
         if (inwin) {
             const uint32_t x = shift + (uint32_t)ho + (lsb >> 3);
             set_in_window(win + t * kSstride, x, lsb, msb, v0);
             dirty |= ((2u << ((x + (msb >> 3) - (lsb >> 3)) >> 4)) - 1u) & ~((1u << (x >> 4)) - 1u);
-            continue;
+            return;
         }
         if (msb - lsb < 64) {
             // outside the window: the same RMW on one 16-byte read of global memory, only the
@@ -494,7 +544,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             uint8_t* h = p.slab + A;
             for (uint32_t j = 0; j < nb; j++)
                 h[j] = (uint8_t)((j < 8 ? W.hi >> (56 - 8 * j) : W.lo >> (120 - 8 * j)) & 0xFFu);
-            continue;
+            return;
         }
         // wider fields (IPv6 addresses): set_bit_range a byte at a time from the field's last byte
         // backwards; bits above the value's 64 become 0
@@ -512,6 +562,13 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             v = nbit >= 64 ? 0 : (v >> nbit);
             b = lo - 1;
         }
+    };
+    if (act) {
+        // the first kPreVals values are loaded in flight together with the windows; the rest per spec
+#pragma unroll
+        for (uint32_t s = 0; s < kPreVals; s++)
+            if (s < p.nspec) apply(s, vpre[s]);
+        for (uint32_t s = kPreVals; s < p.nspec; s++) apply(s, S[s].values[i]);
     }
     // Packet::ipv4_checksum refresh of the csum_occ-th IPv4 header (ipv4_update_kernel's sum) after
     // the setters: header dwords inside the window from LDS, past it from global memory (bytes only
@@ -523,10 +580,15 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             const uint64_t a0 = off & ~(uint64_t)15;  // window byte q <-> slab byte a0 + q
             const uint32_t* w = win + t * kSstride;
             uint32_t d[6];
+            if (inwin && x0 + 24u <= 16u * kSnch) {  // the whole header in the window (the common case)
 #pragma unroll
-            for (int k = 0; k < 6; k++) {
-                const uint32_t q = x0 + 4u * k;
-                d[k] = (inwin && q + 4 <= 16u * kSnch) ? w[q >> 2] : slab_dw(p.b, a0 + q);
+                for (int k = 0; k < 6; k++) d[k] = w[(x0 >> 2) + k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < 6; k++) {
+                    const uint32_t q = x0 + 4u * k;
+                    d[k] = (inwin && q + 4 <= 16u * kSnch) ? w[q >> 2] : slab_dw(p.b, a0 + q);
+                }
             }
             uint32_t sum = 0;
 #pragma unroll
