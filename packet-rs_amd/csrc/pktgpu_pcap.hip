@@ -40,7 +40,11 @@
 
 namespace {
 
-constexpr uint32_t kRegion = 4096;               // bytes of record starts per region
+#ifndef PKTGPU_PCAP_REGION
+#define PKTGPU_PCAP_REGION 4096
+#endif
+constexpr uint32_t kRegion = PKTGPU_PCAP_REGION;  // bytes of record starts per region
+static_assert(kRegion % 16 == 0 && kRegion / 16 <= 65536, "u16 record lists");
 constexpr uint32_t kMaxRec = kRegion / 16;       // records per region (each >= 16 B apart)
 constexpr int kWaves = 4;                         // waves per 256-thread block
 constexpr uint32_t kBlockBytes = kWaves * kRegion;
