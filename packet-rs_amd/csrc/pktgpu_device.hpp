@@ -147,10 +147,25 @@ struct PacketView {
 #pragma unroll
             for (int i = 0; i <= NW; i++) a[i] = wdw(k + i);
         } else {
-            const uint64_t ga = off + b;
+            const uint64_t ga = off + b, g4 = ga & ~(uint64_t)3;
             sh = (uint32_t)(ga & 3);
+            // The header's dwords by 16-byte loads (4-byte aligned: one instruction per 16 bytes
+            // instead of one per dword — separate instructions to one 128-B line each re-request
+            // it from memory); per dword near the slab's readable end.
+            constexpr int NQ = (NW + 1 + 3) / 4;
+            if (g4 + 16u * NQ <= last4 + 4) {
 #pragma unroll
-            for (int i = 0; i <= NW; i++) a[i] = gdw(ga + 4u * i);
+                for (int q = 0; q < NQ; q++) {
+                    uint32_t v[4];
+                    __builtin_memcpy(v, __builtin_assume_aligned(slab + g4 + 16u * q, 4), 16);
+#pragma unroll
+                    for (int j = 0; j < 4; j++)
+                        if (4 * q + j <= NW) a[4 * q + j] = v[j];
+                }
+            } else {
+#pragma unroll
+                for (int i = 0; i <= NW; i++) a[i] = gdw(ga + 4u * i);
+            }
         }
 #pragma unroll
         for (int i = 0; i < NW; i++) d[i] = bswap32(__builtin_amdgcn_alignbyte(a[i + 1], a[i], sh));
