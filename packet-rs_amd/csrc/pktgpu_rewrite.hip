@@ -388,22 +388,46 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
-    // One chunk per lane per round.  (Issuing 4 or 8 rounds' loads before their stores was slower:
-    // C2 45 / 141 vs 33 us, C4 135 / 422 vs 125 us — 120+ VGPRs halve the resident waves,
-    // profiles/ab/r02tv_to_vec_unroll.txt.)
+    // One chunk per lane per round, software-pipelined by one round: the next round's load is
+    // issued before this round's store (a store may alias the next chunk's source, so the
+    // compiler keeps load -> store -> load otherwise: one memory round trip per round).  (Issuing
+    // 4 or 8 rounds' loads ahead was slower: C2 45 / 141 vs 33 us, C4 135 / 422 vs 125 us — 120+
+    // VGPRs halve the resident waves, profiles/ab/r02tv_to_vec_unroll.txt.)
     uint32_t k = 0;
-    for (uint32_t g = lane; g < total; g += 64u) {
+    auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4]) {
         while (s_pre[w][k + 1] <= g) k++;  // packets with no chunks are skipped (pre[64] = total > g)
         const uint64_t s = s_src[w][k], d = s_dst[w][k];
         const uint32_t L = s_len[w][k];
-        const uint64_t ca = (d & ~(uint64_t)15) + 16u * (g - s_pre[w][k]);  // destination chunk
-        uint32_t o[4];
+        ca = (d & ~(uint64_t)15) + 16u * (g - s_pre[w][k]);  // destination chunk
         load_src_chunk(p.b, last16, s, d, ca, o);
-        const uint64_t lo = ca > d ? ca : d, hi = ca + 16 < d + L ? ca + 16 : d + L;
+        lo = ca > d ? ca : d;
+        hi = ca + 16 < d + L ? ca + 16 : d + L;
+    };
+    auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4]) {
         if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
             *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(o[0], o[1], o[2], o[3]);
         } else {
             store_edge_chunk(p.dst, p.dst_len, ca, o, lo, hi);
+        }
+    };
+    if (total <= 4u * 64u) {  // short waves (C2: 4 rounds): the plain loop is faster (33.7 vs 34.4 us)
+        for (uint32_t g = lane; g < total; g += 64u) {
+            uint64_t ca, lo, hi;
+            uint32_t o[4];
+            locate(g, ca, lo, hi, o);
+            put(ca, lo, hi, o);
+        }
+    } else {  // C4: 142 vs 148 us in the input's layout, 124 vs 138 us packed
+        uint64_t ca = 0, lo = 0, hi = 0;
+        uint32_t o[4] = {0, 0, 0, 0};
+        locate(lane, ca, lo, hi, o);  // lane < 256 < total
+        for (uint32_t g = lane; g < total; g += 64u) {
+            uint64_t ca1 = 0, lo1 = 0, hi1 = 0;
+            uint32_t o1[4] = {0, 0, 0, 0};
+            if (g + 64u < total) locate(g + 64u, ca1, lo1, hi1, o1);
+            put(ca, lo, hi, o);
+            ca = ca1, lo = lo1, hi = hi1;
+            o[0] = o1[0], o[1] = o1[1], o[2] = o1[2], o[3] = o1[3];
         }
     }
     // ---- Q2 packets (two or more GRE options), one at a time by the whole wave: output byte q

@@ -7,7 +7,8 @@
                  (MACs, IPs, tos, ttl, id, ports, seq, ack: splitmix64) + the IPv4 checksum refresh
   pktgen_values  the same fields from per-packet value arrays (8 B read per field per packet)
   to_vec_c2 / to_vec_c4   PacketSlice::to_vec of every parsed packet (tests/lib.rs:790-817), C2 slab
-                 and C4 pcap replay, into the input's layout
+                 and C4 pcap replay, into the input's layout; to_vec_c4_packed: the C4 outputs
+                 packed back to back (dst_offsets = prefix of the lengths)
   extract_c2     every field of Ether/IPv4/UDP (19 specs, one launch) over C2 (headers.rs:195-201)
   setfields_c2   4 setters + the IPv4 checksum refresh, in place over C2 (headers.rs:315-324)
 
@@ -219,6 +220,26 @@ def main():
              {"value": round(r * cpu_m / t / 1e9, 6), "unit": "Gpkt/s", "cores": cores, "kind": "port",
               "sample": f"{r} x {cpu_m} records of oracle slow::parse(..).to_vec()"},
              {"parity_vs_oracle_first_20000": bool(ok), "avg_record_bytes": round(avg, 1)})
+        # the same records packed back to back (dst_offsets = prefix of the lengths: each to_vec
+        # output Vec in a contiguous packet buffer, no pcap record headers between them)
+        po = np.zeros(n, np.uint64)
+        po[1:] = np.cumsum(l4[:-1].astype(np.uint64))
+        tot = int(po[-1]) + int(l4[-1])
+        dpo = torch.from_numpy(po).to(dev)
+        dstp = [torch.empty(((tot + 15) // 16) * 16, dtype=torch.uint8, device=dev)
+                for _ in range(max(2, (1 << 30) // tot + 1))]
+        ms = event_ms(lambda k: P.to_vec(d4, ch4, offsets=do4, lens=dl4, dst=dstp[k % len(dstp)], dst_offsets=dpo), it)
+        outp, lnp = P.to_vec(d4, ch4, offsets=do4, lens=dl4, dst=dstp[0], dst_offsets=dpo)
+        op = outp.cpu().numpy()
+        okp = np.array_equal(lnp.cpu().numpy(), wl) and all(
+            np.array_equal(op[int(po[j]):int(po[j]) + int(wl[j])], want_b[int(o4[j]):int(o4[j]) + int(wl[j])])
+            for j in range(0, n, max(1, n // 20000)))
+        line("to_vec_c4_packed", n, ms, round(avg + 8 + 8 + 4 + 1 + 1 + 3 * nh + 4, 1), round(avg + 4, 1),
+             {"value": round(r * cpu_m / t / 1e9, 6), "unit": "Gpkt/s", "cores": cores, "kind": "port",
+              "sample": f"{r} x {cpu_m} records of oracle slow::parse(..).to_vec()"},
+             {"parity_vs_oracle_sampled": bool(okp), "avg_record_bytes": round(avg, 1),
+              "dst": "packed: dst_offsets = prefix of the lengths"})
+        del dstp
         del dsts, d4
     if want("extract_c2"):
         from pktgpu import fields as F

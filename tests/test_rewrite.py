@@ -108,3 +108,30 @@ def test_gpu_set_fields_and_checksum_vs_oracle():
                          n=n, ipv4_checksum=occ, **dkw)
         torch.cuda.synchronize()
         assert np.array_equal(ds2.cpu().numpy(), slab), kind + " fused"
+
+
+@pytest.mark.gpu
+def test_gpu_set_fields_csum_many_specs_vs_oracle():
+    """pkt_set_fields_csum with more than 32 specs (ordered launches; the checksum refresh in the
+    last one) and the inner IPv4 (occurrence 1) on a C4 pcap mix, vs the oracle's setters then
+    Packet::ipv4_checksum."""
+    torch = pytest.importorskip("torch")
+    import pktgpu
+    P = pktgpu.Parser(0)
+    rng = np.random.default_rng(21)
+    slab, offs, lens = gen.gen_c4(20000, seed=22)
+    slab = slab.copy()
+    n = len(offs)
+    kw = dict(offsets=offs, lens=lens)
+    dkw = dict(offsets=torch.from_numpy(offs).cuda(), lens=torch.from_numpy(lens).cuda())
+    ch = oracle.parse_batch(slab, n, columns=["n_hdrs", "hdr_type", "hdr_off"], **kw)
+    base, bvals = _specs_and_values(n, rng)
+    specs = (base * 5)[:41]
+    vals = (bvals * 5)[:41]
+    ds = torch.from_numpy(slab.copy()).cuda()
+    dch = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in ch.items()}
+    P.set_fields(ds, dch, specs, [torch.from_numpy(v).cuda() for v in vals], n=n, ipv4_checksum=1, **dkw)
+    torch.cuda.synchronize()
+    oracle.set_fields(slab, n, ch, specs, vals, **kw)
+    oracle.ipv4_update_checksum(slab, n, ch, 1, **kw)
+    assert np.array_equal(ds.cpu().numpy(), slab)
