@@ -20,6 +20,9 @@
 //                      LDS (one shift and mask on a 16-byte piece), and the chunks holding set bytes
 //                      are stored back cooperatively, the packet's own bytes only; a packet with a
 //                      field past its window or wider than 64 bits is set in global memory instead.
+//                      pkt_set_fields_csum refreshes one IPv4 header's checksum in the same pass.
+//                      (extract / set_fields: spec tables in LDS, every prologue load in flight
+//                      before the first wait: no memory round trip per spec.)
 //   ipv4_update_kernel / ipv4_csum_kernel   Packet::ipv4_checksum (packet.rs:93-107, Q1 fold).
 //   broadcast_kernel   n copies of one packet (the clone step of the pktgen loop).
 #include <hip/hip_runtime.h>
