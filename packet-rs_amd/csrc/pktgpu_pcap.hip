@@ -236,8 +236,13 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     const uint32_t k = blockIdx.x * kWaves + w;
     const uint64_t lbase = (uint64_t)blockIdx.x * kBlockBytes, lend = lbase + kBlockBytes;
     stage<kBlockBytes, 256>(lds, buf, lbase, len, threadIdx.x);
+    // the per-call zeroing the repair rounds rely on (no memset launches): control words 1.. here,
+    // word 0 (the magic) and each region's owner word below
+    if (blockIdx.x == 0)
+        for (uint32_t c = 1 + threadIdx.x; c < kCtlWords; c += 256) S.ctl[c] = 0;
     __syncthreads();
     if (k >= K) return;
+    if (lane == 0) S.own[k] = 0;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     uint16_t* list = lst[w];
     const uint64_t base = (uint64_t)k * kRegion;
@@ -483,9 +488,7 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     S.list = reinterpret_cast<uint16_t*>(p);
 
     const dim3 blk(256);
-    e = hipMemsetAsync(S.ctl, 0, 8ull * kCtlWords, s);
-    if (e == hipSuccess) e = hipMemsetAsync(S.own, 0, 4ull * K, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
+    // (the guess kernel zeroes the control words and the owner words)
     hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap guess launch");
     // Each pass: two repair rounds, then the scan and the emit on speculation, and ONE read-back.
