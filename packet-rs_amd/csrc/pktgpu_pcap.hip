@@ -52,7 +52,11 @@ constexpr uint32_t kScanBlock = 1024;             // regions per first-level sca
 constexpr uint32_t kEmitRegions = 16;             // regions per emit block
 constexpr int kLookback = 64;                     // empty regions skipped when finding an entry
 constexpr int kChaseMax = 256;                    // regions one repair chase may rewrite
-constexpr int kMinHops = 3, kMaxHops = 4;         // guess chain length
+#ifndef PKTGPU_PCAP_HOPS
+#define PKTGPU_PCAP_HOPS 2, 2  // (min, max); 3, 4: 117 us per call, 2, 3: 112, 2, 2: 108 (profiles/ab/r02hops_*)
+#endif
+constexpr int kHops[2] = {PKTGPU_PCAP_HOPS};
+constexpr int kMinHops = kHops[0], kMaxHops = kHops[1];  // guess chain length
 constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec within a day
 constexpr uint32_t kPassSlots = 64;               // passes with their own control words
 

@@ -18,8 +18,8 @@ def u32(b, o):
         (bytes(b[o:o + 4]) + b"\0\0\0\0")[:4], "little")
 
 
-MIN_HOPS = 3
-MAX_HOPS = 4
+MIN_HOPS = 2  # PKTGPU_PCAP_HOPS (pktgpu_pcap.hip)
+MAX_HOPS = 2
 CHASE_MAX = 256
 ORIG_MAX = 1 << 20
 TS_SPAN = 86400
