@@ -41,6 +41,7 @@ __constant__ uint8_t kHdrSize[PKT_HDR_COUNT] = {0, 14, 4, 20, 40, 4, 20, 8, 28, 
 
 constexpr uint32_t kRwBlock = 256;
 constexpr int kMaxSpecs = 32;  // specs per launch (extract / set_fields)
+static_assert(kRwBlock >= (uint32_t)kMaxSpecs, "one thread copies each spec into the LDS spec table");
 
 struct BatchRef {
     const uint8_t* slab;
