@@ -94,6 +94,9 @@ __device__ __forceinline__ uint32_t gre_next(uint32_t p) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // A lane's view of its packet: LDS window + global fallback.
+#ifndef PKTGPU_LDS_UNALIGNED
+#define PKTGPU_LDS_UNALIGNED 1  // window reads as unaligned LDS loads (gfx950 unaligned-ds-access), not dword pairs + v_alignbyte: C2 isolated 28.9 -> 27.3 us (profiles/ab/r02ulds_unaligned_lds.txt)
+#endif
 struct PacketView {
     const uint8_t* lw;        // LDS window of this packet (dword-aligned)
     const uint8_t* slab;      // slab base (16-byte aligned)
@@ -117,6 +120,13 @@ struct PacketView {
     // n (1..4) bytes at packet offset b, little-endian in the low bytes (garbage above n).
     // Caller guarantees b + n <= len.  Bytes past the window come from global memory (L2).
     __device__ __forceinline__ uint32_t le(uint32_t b, uint32_t n) const {
+#if PKTGPU_LDS_UNALIGNED
+        if (b >= win_lo && b + n <= win_end) {  // (a window is followed by >= 4 readable LDS bytes)
+            uint32_t v;
+            __builtin_memcpy(&v, lw + (uint32_t)(b + shift), 4);
+            return v;
+        }
+#endif
         if (b >= win_lo && b + n <= win_end) {
             uint32_t wb = b + shift;
             uint32_t k = wb >> 2, sh = wb & 3;
@@ -141,11 +151,20 @@ struct PacketView {
         uint32_t a[NW + 1];
         uint32_t sh;
         if (b >= win_lo && b + 4 * NW <= win_end) {
+#if PKTGPU_LDS_UNALIGNED
+            // unaligned LDS reads (gfx950 unaligned-ds-access): the header's bytes as they lie
+            uint32_t u[NW];
+            __builtin_memcpy(u, lw + (uint32_t)(b + shift), 4 * NW);
+#pragma unroll
+            for (int i = 0; i < NW; i++) d[i] = bswap32(u[i]);
+            return;
+#else
             const uint32_t wb = b + shift;
             const uint32_t k = wb >> 2;
             sh = wb & 3;
 #pragma unroll
             for (int i = 0; i <= NW; i++) a[i] = wdw(k + i);
+#endif
         } else {
             const uint64_t ga = off + b, g4 = ga & ~(uint64_t)3;
             sh = (uint32_t)(ga & 3);
