@@ -95,7 +95,10 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 
 // A lane's view of its packet: LDS window + global fallback.
 #ifndef PKTGPU_LDS_UNALIGNED
-#define PKTGPU_LDS_UNALIGNED 1  // window reads as unaligned LDS loads (gfx950 unaligned-ds-access), not dword pairs + v_alignbyte: C2 isolated 28.9 -> 27.3 us (profiles/ab/r02ulds_unaligned_lds.txt)
+// hdr<>'s window reads as unaligned LDS loads (gfx950 unaligned-ds-access), not dword pairs +
+// v_alignbyte: C2 isolated 28.9 -> 27.3 us (profiles/ab/r02ulds_unaligned_lds.txt).  le() keeps
+// the dword pair: as one unaligned load it made extract_kernel's 19 getters 68.6 -> 79.5 us.
+#define PKTGPU_LDS_UNALIGNED 1
 #endif
 struct PacketView {
     const uint8_t* lw;        // LDS window of this packet (dword-aligned)
@@ -120,13 +123,6 @@ struct PacketView {
     // n (1..4) bytes at packet offset b, little-endian in the low bytes (garbage above n).
     // Caller guarantees b + n <= len.  Bytes past the window come from global memory (L2).
     __device__ __forceinline__ uint32_t le(uint32_t b, uint32_t n) const {
-#if PKTGPU_LDS_UNALIGNED
-        if (b >= win_lo && b + n <= win_end) {  // (a window is followed by >= 4 readable LDS bytes)
-            uint32_t v;
-            __builtin_memcpy(&v, lw + (uint32_t)(b + shift), 4);
-            return v;
-        }
-#endif
         if (b >= win_lo && b + n <= win_end) {
             uint32_t wb = b + shift;
             uint32_t k = wb >> 2, sh = wb & 3;
