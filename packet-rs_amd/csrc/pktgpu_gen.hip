@@ -13,10 +13,13 @@
 // (headers.rs:315-324: the field's bits get the value's low `width` bits, bit `end` the value's
 // bit 0) by one shift and mask.
 //
-//   gen_region_kernel (fields or checksums, stride <= 1 KiB): one lane per packet; the wave's 64
-//   packets are built in LDS (template, then each field applied once per packet to the 1-2 pieces
-//   it overlaps, then Packet::ipv4_checksum (packet.rs:93-107, Q1 fold) of each refreshed IPv4
-//   header read back from the row, as the builders do, utils.rs:233-236), then stored.
+//   gen_region_kernel (fields or checksums, stride <= 1 KiB): one lane per packet; the pieces of
+//   the wave's 64 packets that a field or checksum touches are built in LDS (template, then each
+//   field applied once per packet to the 1-2 pieces it overlaps, then Packet::ipv4_checksum
+//   (packet.rs:93-107, Q1 fold) of each refreshed IPv4 header read back from the row, as the
+//   builders do, utils.rs:233-236), then the packets are stored, untouched pieces straight from
+//   the template (test_tcp_packet: 3 of 10 pieces in LDS; 11 fields + checksum 53 -> 42 us,
+//   profiles/ab/r02gendirty_pktgen_touched_pieces.txt).
 //   gen_kernel (pure clones, wider strides): one lane per 16-byte piece; a lane applies the fields
 //   overlapping its piece and, if it holds checksum bytes, rebuilds that IPv4 header's pieces.
 // Measured on test_tcp_packet (154 B, stride 160), 2^20 packets: clone 27 us (gen_kernel) / 30.5 us
@@ -41,7 +44,7 @@ namespace {
 constexpr int kMaxGenFields = 32;
 constexpr int kMaxGenCsum = 8;
 constexpr uint32_t kGenBlock = 256;
-constexpr uint32_t kRegionMaxStride = 1024;  // gen_region_kernel: 64 * stride bytes of LDS per wave
+constexpr uint32_t kRegionMaxStride = 1024;  // gen_region_kernel: strides up to 64 pieces (LDS: 64 x the touched pieces)
 // pieces per launch: lane indices stay 32-bit (a launch covers whole packets)
 constexpr uint64_t kGenChunkPieces = 1ull << 31;
 
@@ -59,6 +62,9 @@ struct GenParams {
     uint64_t first;       // global index of this launch's first packet (INC / RANDOM)
     uint32_t tpl_bytes;
     uint32_t ppp;         // 16-byte pieces per packet = stride / 16
+    uint32_t nd;          // gen_region_kernel: pieces a field or checksum touches (staged in LDS)
+    uint32_t pk_magic;    // ceil(2^20 / ppp): packet of output piece q = (q * pk_magic) >> 20
+    int8_t slot[64];      // piece -> its LDS slot in the packet's row, -1 = the template's bytes
     uint32_t npieces;     // pieces of this launch (gen_kernel)
     uint32_t npkts;       // packets of this launch (gen_region_kernel)
     uint32_t nf, ncs;
@@ -168,31 +174,38 @@ __device__ __forceinline__ void lds_put(uint8_t* at, const U128& x) {
 
 __global__ __launch_bounds__(64) void gen_region_kernel(GenParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t region[];
+    __shared__ uint4 tp[64];      // the template's pieces (zeros past it)
+    __shared__ int32_t sl[64];    // piece -> slot
     const uint32_t lane = threadIdx.x;
     const uint32_t w0 = blockIdx.x * 64u;
     const uint32_t i = w0 + lane;
     const bool act = i < p.npkts;
     const uint64_t g = p.first + i;
     const uint32_t stride = p.ppp * 16u;
-    uint8_t* row = region + lane * stride;
-    for (uint32_t k = 0; k < p.ppp; k++) {  // the template (zeros past it)
-        uint4 t = make_uint4(0, 0, 0, 0);
-        if (k * 16u < p.tpl_bytes) t = *reinterpret_cast<const uint4*>(p.tpl + k * 16u);
-        *reinterpret_cast<uint4*>(row + k * 16u) = t;
+    if (lane < p.ppp) {
+        tp[lane] = lane * 16u < p.tpl_bytes ? *reinterpret_cast<const uint4*>(p.tpl + lane * 16u) : make_uint4(0, 0, 0, 0);
+        sl[lane] = p.slot[lane];
     }
+    __syncthreads();
+    // Only the pieces a field or a checksum touches are built in LDS (the row holds nd of them);
+    // the rest of each packet is the template, stored straight from `tp`.
+    uint8_t* row = region + lane * p.nd * 16u;
+    for (uint32_t k = 0; k < p.ppp; k++)
+        if (sl[k] >= 0) *reinterpret_cast<uint4*>(row + sl[k] * 16u) = tp[k];
     for (uint32_t j = 0; j < p.nf; j++) {  // fields in order (uniform)
         const GenField& f = p.f[j];
         const uint64_t v = act ? field_value(f, i, g) : 0;
         for (uint32_t k = f.s >> 7; k <= (f.e >> 7); k++) {
-            U128 x = lds_get(row + k * 16u);
+            uint8_t* at = row + sl[k] * 16u;
+            U128 x = lds_get(at);
             put_bits(x, f.s, f.e, f.w, v, k * 128u);
-            lds_put(row + k * 16u, x);
+            lds_put(at, x);
         }
     }
     for (uint32_t c = 0; c < p.ncs; c++) {  // checksums last (uniform)
         const uint32_t hb = p.csum_at[c], k0 = hb >> 4, r = hb & 15u;
-        const U128 x0 = lds_get(row + k0 * 16u), x1 = lds_get(row + k0 * 16u + 16u);
-        const U128 x2 = r + 20u > 32u ? lds_get(row + k0 * 16u + 32u) : U128{0, 0};
+        const U128 x0 = lds_get(row + sl[k0] * 16u), x1 = lds_get(row + sl[k0 + 1] * 16u);
+        const U128 x2 = r + 20u > 32u ? lds_get(row + sl[k0 + 2] * 16u) : U128{0, 0};
         uint32_t sum = 0;
 #pragma unroll
         for (uint32_t j = 0; j < 20; j += 2)
@@ -200,19 +213,24 @@ __global__ __launch_bounds__(64) void gen_region_kernel(GenParams p) {
         const uint32_t cv = ~(((sum >> 16) + sum) & 0xFFFFu) & 0xFFFFu;  // packet.rs:102-104 (Q1)
         const uint32_t cb = hb + 10u;
         for (uint32_t k = cb >> 4; k <= ((cb + 1u) >> 4); k++) {
-            U128 x = lds_get(row + k * 16u);
+            uint8_t* at = row + sl[k] * 16u;
+            U128 x = lds_get(at);
             put_bits(x, cb * 8u, cb * 8u + 15u, 16u, cv, k * 128u);
-            lds_put(row + k * 16u, x);
+            lds_put(at, x);
         }
     }
     __syncthreads();
     const uint32_t npk = p.npkts - w0 < 64u ? p.npkts - w0 : 64u;
     const uint32_t bytes = npk * stride;
     uint8_t* d = p.dst + (uint64_t)w0 * stride;
-    for (uint32_t o = lane * 16u; o < bytes; o += 1024u)
-        *reinterpret_cast<uint4*>(d + o) = *reinterpret_cast<const uint4*>(region + o);
+    // the wave's packets as consecutive 1 KiB per store instruction: output piece q is piece k of
+    // packet pk, from its LDS slot or the template
+    for (uint32_t o = lane * 16u; o < bytes; o += 1024u) {
+        const uint32_t q = o >> 4, pk = (q * p.pk_magic) >> 20, k = q - pk * p.ppp;
+        const int32_t sk = sl[k];
+        *reinterpret_cast<uint4*>(d + o) = sk >= 0 ? *reinterpret_cast<const uint4*>(region + (pk * p.nd + (uint32_t)sk) * 16u) : tp[k];
+    }
 }
-
 }  // namespace
 
 struct pkt_gen {
@@ -362,6 +380,16 @@ int pkt_gen_run(pkt_gen_t* g, uint64_t first, uint64_t n, uint32_t stride, const
     p.nf = (uint32_t)g->fields.size();
     p.ncs = (uint32_t)g->csum_at.size();
     for (uint32_t c = 0; c < p.ncs; c++) p.csum_at[c] = g->csum_at[c];
+    // the pieces a field or a checksum (its whole 20-byte header) touches, for the region kernel
+    bool dirty[64] = {};
+    if (p.ppp <= 64) {
+        for (const GenField& f : g->fields)
+            for (uint32_t k = f.s >> 7; k <= (f.e >> 7) && k < 64; k++) dirty[k] = true;
+        for (uint32_t c = 0; c < p.ncs; c++)
+            for (uint32_t k = p.csum_at[c] >> 4; k <= ((p.csum_at[c] + 19u) >> 4) && k < 64; k++) dirty[k] = true;
+        for (uint32_t k = 0; k < 64; k++) p.slot[k] = (k < p.ppp && dirty[k]) ? (int8_t)p.nd++ : (int8_t)-1;
+    }
+    p.pk_magic = ((1u << 20) + p.ppp - 1) / p.ppp;
     const uint64_t per = std::max<uint64_t>(1, kGenChunkPieces / p.ppp);  // packets per launch
     for (uint64_t i0 = 0; i0 < n; i0 += per) {
         const uint64_t m = std::min(per, n - i0);
@@ -376,7 +404,7 @@ int pkt_gen_run(pkt_gen_t* g, uint64_t first, uint64_t n, uint32_t stride, const
         // region kernel whenever a field or checksum is applied and the 64-packet region fits LDS;
         // pure clones (and strides over 1 KiB) take the lane-per-piece kernel
         if ((p.nf || p.ncs) && stride <= kRegionMaxStride)
-            hipLaunchKernelGGL(gen_region_kernel, dim3((p.npkts + 63) / 64), dim3(64), 64 * stride,
+            hipLaunchKernelGGL(gen_region_kernel, dim3((p.npkts + 63) / 64), dim3(64), 64u * 16u * p.nd,
                                reinterpret_cast<hipStream_t>(stream), p);
         else
             hipLaunchKernelGGL(gen_kernel, dim3((p.npieces + kGenBlock - 1) / kGenBlock), dim3(kGenBlock), 0,
