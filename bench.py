@@ -527,6 +527,9 @@ def main():
             "file": f"profiles/traffic_{args.config}.json",
             "how": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes of "
                    "this bench command (scripts/gpu_round.sh)",
+            "x2_check": "every memory-side read request of these launches is a 128-B line "
+                        "(TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; FETCH_SIZE counts 64 B per request): "
+                        "profiles/ab/r02calib_fetch_requests.txt",
             "run": t.get("label", "")}
     if c5 is not None:
         res["c5"] = c5
