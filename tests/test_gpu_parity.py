@@ -161,6 +161,19 @@ def test_c2_chain_only_and_subsets(P):
         both(P, slab, n, stride=64, columns=cols, label=str(cols))
 
 
+def test_c4_chain_only_and_subsets(P):
+    """Indexed batches with column subsets (chain-only, status-only, chain + one header group,
+    status + one field group: the runtime-checked kernel and the chain kernel) vs the oracle, and
+    the ref22 capture (every template, every alignment phase) with the chain columns."""
+    n = 1 << 18
+    buf, offs, lens = gen.gen_c4(n, seed=44)
+    for cols in (["chain"], ["status", "payload_len"], ["chain", "ipv6"], ["status", "udp"]):
+        both(P, buf, n, offsets=offs, lens=lens, columns=cols, label=f"c4 {cols}")
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    o22, l22 = gen.pcap_index_py(pc)
+    both(P, np.frombuffer(pc, np.uint8), 22, offsets=o22, lens=l22, columns=["chain"], label="ref22 chain")
+
+
 # ------------------------------------------------------------------ entries and edge cases
 @pytest.mark.parametrize("entry", schema.ENTRIES)
 def test_entries_random_and_templates(P, entry):
