@@ -140,12 +140,13 @@ struct XParams {
     XSpec s[kMaxSpecs];
 };
 
-// Window of a lane's packet: its first kXnch aligned 16-byte chunks, in LDS at an odd dword stride
-// (per-lane dword reads conflict-free); bytes past it come from global memory (PacketView).
-constexpr int kXnch = 5;
-constexpr uint32_t kXstride = 4 * kXnch + 1;  // dwords
+// Window of a lane's packet: its first NCH aligned 16-byte chunks, in LDS at an odd dword stride
+// (per-lane dword reads conflict-free); bytes past it come from global memory (PacketView).  NCH =
+// 4 for fixed-stride batches of <= 64-byte slots (a fifth chunk would be the next packet's), else 5.
 
+template <int NCH>
 __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
+    constexpr uint32_t kXstride = 4 * NCH + 1;  // dwords
     __shared__ ChainLds L;
     __shared__ uint32_t win[kRwBlock * kXstride];
     // The spec table in LDS: indexed by the loop counter, the kernel-argument copy is read with a
@@ -158,12 +159,12 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
     uint32_t* w = win + t * kXstride;
     // cooperative window loads, issued before the chain is staged so that both are in flight
-    // together: the wave's 64 windows as 64*kXnch (packet, chunk) pairs, pair 64k + lane in load k
+    // together: the wave's 64 windows as 64*NCH (packet, chunk) pairs, pair 64k + lane in load k
     // (consecutive lanes, consecutive chunks of one packet, as in the parse kernel)
-    uint4 v[kXnch];
+    uint4 v[NCH];
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kXnch; k++) {
-        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kXnch, c = pid % (uint32_t)kXnch;
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
         uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
@@ -177,8 +178,8 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     // every load above is in flight; now the LDS stores
     if (t < p.nspec) S[t] = xs;
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kXnch; k++) {
-        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kXnch, c = pid % (uint32_t)kXnch;
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
         uint32_t* wr = win + (wave0 + r) * kXstride + 4 * c;
         wr[0] = v[k].x, wr[1] = v[k].y, wr[2] = v[k].z, wr[3] = v[k].w;
     }
@@ -192,7 +193,7 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     pv.last4 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 4;
     pv.shift = (uint32_t)(off & 15);
     pv.win_lo = 0;
-    pv.win_end = 16u * kXnch - pv.shift;
+    pv.win_end = 16u * NCH - pv.shift;
     pv.len = 0xFFFFFFFFu;  // (le() does not use it)
     uint32_t last_ty = 0xFFFFFFFFu, last_occ = 0;
     int32_t ho = -1;
@@ -468,10 +469,8 @@ struct SParams {
     SSpec s[kMaxSpecs];
 };
 
-// The packet's first kSnch 16-byte chunks (from its 16-byte-aligned start) in LDS at an odd
-// dword stride, as in the parse kernel.
-constexpr int kSnch = 5;
-constexpr uint32_t kSstride = 4 * kSnch + 1;  // dwords
+// The packet's first NCH 16-byte chunks (from its 16-byte-aligned start) in LDS at an odd dword
+// stride, as in the parse kernel (NCH as in extract_kernel).
 constexpr uint32_t kPreVals = 4;  // setter values prefetched into registers
 
 // One setter on a <= 64-bit field whose bytes start at byte x of the lane's LDS window: its <= 9
@@ -489,7 +488,9 @@ __device__ __forceinline__ void set_in_window(uint32_t* w, uint32_t x, uint32_t 
     for (uint32_t j = 0; j < nb; j++) h[j] = (uint8_t)((j < 8 ? W.hi >> (56 - 8 * j) : W.lo >> (120 - 8 * j)) & 0xFFu);
 }
 
+template <int NCH>
 __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
+    constexpr uint32_t kSstride = 4 * NCH + 1;  // dwords
     __shared__ ChainLds L;
     __shared__ uint32_t win[kRwBlock * kSstride + 8];  // +8: the last lane's 16-byte over-read
     __shared__ SSpec S[kMaxSpecs];  // the spec table in LDS (as in extract_kernel)
@@ -505,14 +506,14 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
         plen = (uint64_t)plen > room ? (uint32_t)room : plen;
     }
     // All loads first, in flight together: the windows (cooperative: the wave's 64 windows as
-    // 64*kSnch (packet, chunk) pairs, pair 64k + lane in load k, so each window comes from one or
+    // 64*NCH (packet, chunk) pairs, pair 64k + lane in load k, so each window comes from one or
     // two wave instructions, as in the parse kernel), the chain, the first kPreVals values (their
     // pointers are kernel arguments at constant indices: scalar loads) and the spec table.
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
-    uint4 v[kSnch];
+    uint4 v[NCH];
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
-        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
         uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
@@ -528,8 +529,8 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     if (t < p.nspec) ss = p.s[t];
     if (t < p.nspec) S[t] = ss;
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
-        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
         uint32_t* w = win + (wave0 + r) * kSstride + 4 * c;
         w[0] = v[k].x, w[1] = v[k].y, w[2] = v[k].z, w[3] = v[k].w;
     }
@@ -541,7 +542,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     for (uint32_t s = 0; s < p.nspec && inwin; s++) {
         const pkt_field_spec_t sp = S[s].f;
         const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
-        if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * kSnch)) inwin = false;
+        if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * NCH)) inwin = false;
     }
     uint32_t dirty = 0;  // window chunks holding a set byte
     // one setter (specs in order: overlapping ones act as sequential setters)
@@ -608,14 +609,14 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             const uint64_t a0 = off & ~(uint64_t)15;  // window byte q <-> slab byte a0 + q
             const uint32_t* w = win + t * kSstride;
             uint32_t d[6];
-            if (inwin && x0 + 24u <= 16u * kSnch) {  // the whole header in the window (the common case)
+            if (inwin && x0 + 24u <= 16u * NCH) {  // the whole header in the window (the common case)
 #pragma unroll
                 for (int k = 0; k < 6; k++) d[k] = w[(x0 >> 2) + k];
             } else {
 #pragma unroll
                 for (int k = 0; k < 6; k++) {
                     const uint32_t q = x0 + 4u * k;
-                    d[k] = (inwin && q + 4 <= 16u * kSnch) ? w[q >> 2] : slab_dw(p.b, a0 + q);
+                    d[k] = (inwin && q + 4 <= 16u * NCH) ? w[q >> 2] : slab_dw(p.b, a0 + q);
                 }
             }
             uint32_t sum = 0;
@@ -630,7 +631,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
             for (uint32_t j = 0; j < 2; j++) {
                 const uint32_t q = x + 10u + j;
                 const uint8_t byte = (uint8_t)(j ? c : c >> 8);
-                if (inwin && q < 16u * kSnch) {
+                if (inwin && q < 16u * NCH) {
                     reinterpret_cast<uint8_t*>(win + t * kSstride)[q] = byte;
                     dirty |= 1u << (q >> 4);
                 } else {
@@ -644,8 +645,8 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     // write back the dirty chunks, the packet's own bytes only, with the pairs of the loads
 #pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)kSnch; k++) {
-        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)kSnch, c = pid % (uint32_t)kSnch;
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + lane, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
         const uint32_t dr = (uint32_t)__shfl((int)dirty, (int)r, 64);
         const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                               (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
@@ -720,6 +721,9 @@ __global__ __launch_bounds__(kRwBlock) void ipv4_csum_kernel(const uint8_t* hdrs
     out[i] = (uint16_t)~s;
 }
 
+// Fixed-stride batches of <= 64-byte, 16-byte-aligned slots: 4-chunk windows (the packet) instead of 5.
+bool narrow_slots(const pkt_batch_t* b) { return !b->offsets && b->stride <= 64 && b->stride % 16 == 0; }
+
 int batch_ref(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* chain, BatchRef& r) {
     if (!b->slab || !chain || !chain->n_hdrs || !chain->hdr_type || !chain->hdr_off)
         return fail(ctx, PKT_ERR_INVALID_ARG, "null slab/chain column");
@@ -781,7 +785,10 @@ int pkt_extract_fields(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t* 
             xp.s[k].values = values[q];
             xp.s[k].found = found ? found[q] : nullptr;
         }
-        hipLaunchKernelGGL(extract_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), xp);
+        if (narrow_slots(b))
+            hipLaunchKernelGGL(extract_kernel<4>, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), xp);
+        else
+            hipLaunchKernelGGL(extract_kernel<5>, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), xp);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "extract_kernel launch");
     }
     return PKT_SUCCESS;
@@ -835,7 +842,10 @@ int pkt_set_fields_csum(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_chain_t*
             sp.s[k].f = specs[s0 + k];
             sp.s[k].values = values[s0 + k];
         }
-        hipLaunchKernelGGL(set_fields_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), sp);
+        if (narrow_slots(b))
+            hipLaunchKernelGGL(set_fields_kernel<4>, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), sp);
+        else
+            hipLaunchKernelGGL(set_fields_kernel<5>, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), sp);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "set_fields_kernel launch");
         s0 += sp.nspec;
     } while (s0 < nspec);

@@ -135,3 +135,24 @@ def test_gpu_set_fields_csum_many_specs_vs_oracle():
     oracle.set_fields(slab, n, ch, specs, vals, **kw)
     oracle.ipv4_update_checksum(slab, n, ch, 1, **kw)
     assert np.array_equal(ds.cpu().numpy(), slab)
+
+
+@pytest.mark.gpu
+def test_gpu_extract_narrow_slots_vs_oracle():
+    """Fixed-stride slabs of <= 64-byte slots take 4-chunk windows in extract / set_fields (a fifth
+    chunk would be the next packet's): every Ether/IPv4/UDP getter on C2 at its 64-byte stride."""
+    torch = pytest.importorskip("torch")
+    import pktgpu
+    from pktgpu import fields as F
+    P = pktgpu.Parser(0)
+    n = 30000
+    slab = gen.gen_c2(n, seed=31).reshape(-1).copy()
+    ch = oracle.parse_batch(slab, n, columns=["n_hdrs", "hdr_type", "hdr_off"], stride=64)
+    specs = [(H[h], 0, s0, e0) for h in ("Ether", "IPv4", "UDP") for (s0, e0) in F.FIELDS[H[h]].values()]
+    dch = {k: torch.from_numpy(np.ascontiguousarray(v)).cuda() for k, v in ch.items()}
+    vals, found = P.extract_fields(torch.from_numpy(slab).cuda(), dch, specs, stride=64)
+    torch.cuda.synchronize()
+    ov, of = oracle.extract_fields(slab, n, ch, specs, stride=64)
+    for k, sp in enumerate(specs):
+        assert np.array_equal(vals[k].cpu().numpy(), ov[k]), sp
+        assert np.array_equal(found[k].cpu().numpy(), of[k]), sp
