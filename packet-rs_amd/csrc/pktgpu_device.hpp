@@ -164,9 +164,10 @@ struct PacketView {
         } else {
             const uint64_t ga = off + b, g4 = ga & ~(uint64_t)3;
             sh = (uint32_t)(ga & 3);
-            // The header's dwords by 16-byte loads (4-byte aligned: one instruction per 16 bytes
-            // instead of one per dword — separate instructions to one 128-B line each re-request
-            // it from memory); per dword near the slab's readable end.
+            // The header's dwords by 16-byte loads (4-byte aligned: one instruction and one wait
+            // per 16 bytes instead of per dword; C4 pipelined -2..-4 %, the line-request count is
+            // unchanged, profiles/ab/r02hv_header_vector_loads.txt); per dword near the slab's
+            // readable end.
             constexpr int NQ = (NW + 1 + 3) / 4;
             if (g4 + 16u * NQ <= last4 + 4) {
 #pragma unroll
