@@ -26,7 +26,12 @@ namespace {
 // requested (no per-column checks at all), or GM = G_RUNTIME (each column checked for NULL).
 enum : uint32_t {
     G_CHAIN = 1, G_ETHER = 2, G_VLAN = 4, G_IPV4 = 8, G_IPV6 = 16, G_TCP = 32, G_UDP = 64,
-    G_ALL = 127, G_RUNTIME = 128
+    G_ALL = 127, G_RUNTIME = 128,
+    // flag: store the columns non-temporally.  Set for the indexed-batch (lockstep) kernels: C4
+    // isolated 105 -> 98 us, pipelined 86 -> 82.5 us, line requests 2.39M -> 2.29M (the columns
+    // no longer evict the records' lines from L2); fixed-stride C2 keeps plain stores (pipelined
+    // +0.3 us with them), profiles/ab/r02ntst_nt_column_stores.txt
+    G_NT = 256
 };
 
 template <uint32_t GM, uint32_t G>
@@ -36,13 +41,11 @@ __device__ __forceinline__ bool want(const void* p) {
 }
 
 // Store at a 32-bit byte offset from a column base (global_store ... saddr: one VGPR offset).
-template <class T>
+template <bool NT, class T>
 __device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
-#if PKTGPU_NT_STORE
-    if constexpr (std::is_integral<T>::value)
+    if constexpr (NT && std::is_integral<T>::value)
         __builtin_nontemporal_store(v, reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff));
     else
-#endif
         *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff) = v;
 }
 
@@ -58,19 +61,19 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         uint32_t d[4] = {0, 0, 0, 0};
         const bool h = ok && r.f_eth >= 0;
         if (h) pv.template hdr<4>((uint32_t)r.f_eth, 14, d);
-        if (want<GM, G_ETHER>(out.eth_dst)) st<uint64_t>(out.eth_dst, o8, ((uint64_t)d[0] << 16) | (d[1] >> 16));
-        if (want<GM, G_ETHER>(out.eth_src)) st<uint64_t>(out.eth_src, o8, ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[2]);
-        if (want<GM, G_ETHER>(out.eth_etype)) st<uint16_t>(out.eth_etype, o2, (uint16_t)(d[3] >> 16));
+        if (want<GM, G_ETHER>(out.eth_dst)) st<(GM & G_NT) != 0, uint64_t>(out.eth_dst, o8, ((uint64_t)d[0] << 16) | (d[1] >> 16));
+        if (want<GM, G_ETHER>(out.eth_src)) st<(GM & G_NT) != 0, uint64_t>(out.eth_src, o8, ((uint64_t)(d[1] & 0xFFFFu) << 32) | d[2]);
+        if (want<GM, G_ETHER>(out.eth_etype)) st<(GM & G_NT) != 0, uint16_t>(out.eth_etype, o2, (uint16_t)(d[3] >> 16));
     }
     // Vlan (headers.rs:543-552): pcp 0-2, cfi 3, vid 4-15, etype 16-31
     if (want<GM, G_VLAN>(out.vlan_pcp) || want<GM, G_VLAN>(out.vlan_cfi) || want<GM, G_VLAN>(out.vlan_vid) ||
         want<GM, G_VLAN>(out.vlan_etype)) {
         uint32_t d[1] = {0};
         if (ok && r.f_vlan >= 0) pv.template hdr<1>((uint32_t)r.f_vlan, 4, d);
-        if (want<GM, G_VLAN>(out.vlan_pcp)) st<uint8_t>(out.vlan_pcp, o1, (uint8_t)(d[0] >> 29));
-        if (want<GM, G_VLAN>(out.vlan_cfi)) st<uint8_t>(out.vlan_cfi, o1, (uint8_t)((d[0] >> 28) & 1u));
-        if (want<GM, G_VLAN>(out.vlan_vid)) st<uint16_t>(out.vlan_vid, o2, (uint16_t)((d[0] >> 16) & 0xFFFu));
-        if (want<GM, G_VLAN>(out.vlan_etype)) st<uint16_t>(out.vlan_etype, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_VLAN>(out.vlan_pcp)) st<(GM & G_NT) != 0, uint8_t>(out.vlan_pcp, o1, (uint8_t)(d[0] >> 29));
+        if (want<GM, G_VLAN>(out.vlan_cfi)) st<(GM & G_NT) != 0, uint8_t>(out.vlan_cfi, o1, (uint8_t)((d[0] >> 28) & 1u));
+        if (want<GM, G_VLAN>(out.vlan_vid)) st<(GM & G_NT) != 0, uint16_t>(out.vlan_vid, o2, (uint16_t)((d[0] >> 16) & 0xFFFu));
+        if (want<GM, G_VLAN>(out.vlan_etype)) st<(GM & G_NT) != 0, uint16_t>(out.vlan_etype, o2, (uint16_t)(d[0] & 0xFFFFu));
     }
     // IPv4 (headers.rs:555-574) + Packet::ipv4_checksum (packet.rs:93-107)
     if (want<GM, G_IPV4>(out.ipv4_version) || want<GM, G_IPV4>(out.ipv4_ihl) || want<GM, G_IPV4>(out.ipv4_diffserv) ||
@@ -81,24 +84,24 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         uint32_t d[5] = {0, 0, 0, 0, 0};
         const bool h = ok && r.f_ipv4 >= 0;
         if (h) pv.template hdr<5>((uint32_t)r.f_ipv4, 20, d);
-        if (want<GM, G_IPV4>(out.ipv4_version)) st<uint8_t>(out.ipv4_version, o1, (uint8_t)(d[0] >> 28));
-        if (want<GM, G_IPV4>(out.ipv4_ihl)) st<uint8_t>(out.ipv4_ihl, o1, (uint8_t)((d[0] >> 24) & 0xFu));
-        if (want<GM, G_IPV4>(out.ipv4_diffserv)) st<uint8_t>(out.ipv4_diffserv, o1, (uint8_t)((d[0] >> 16) & 0xFFu));
-        if (want<GM, G_IPV4>(out.ipv4_total_len)) st<uint16_t>(out.ipv4_total_len, o2, (uint16_t)(d[0] & 0xFFFFu));
-        if (want<GM, G_IPV4>(out.ipv4_identification)) st<uint16_t>(out.ipv4_identification, o2, (uint16_t)(d[1] >> 16));
-        if (want<GM, G_IPV4>(out.ipv4_flags)) st<uint8_t>(out.ipv4_flags, o1, (uint8_t)((d[1] >> 13) & 7u));
-        if (want<GM, G_IPV4>(out.ipv4_frag_startset)) st<uint16_t>(out.ipv4_frag_startset, o2, (uint16_t)(d[1] & 0x1FFFu));
-        if (want<GM, G_IPV4>(out.ipv4_ttl)) st<uint8_t>(out.ipv4_ttl, o1, (uint8_t)(d[2] >> 24));
-        if (want<GM, G_IPV4>(out.ipv4_protocol)) st<uint8_t>(out.ipv4_protocol, o1, (uint8_t)((d[2] >> 16) & 0xFFu));
-        if (want<GM, G_IPV4>(out.ipv4_header_checksum)) st<uint16_t>(out.ipv4_header_checksum, o2, (uint16_t)(d[2] & 0xFFFFu));
-        if (want<GM, G_IPV4>(out.ipv4_src)) st<uint32_t>(out.ipv4_src, o4, d[3]);
-        if (want<GM, G_IPV4>(out.ipv4_dst)) st<uint32_t>(out.ipv4_dst, o4, d[4]);
+        if (want<GM, G_IPV4>(out.ipv4_version)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_version, o1, (uint8_t)(d[0] >> 28));
+        if (want<GM, G_IPV4>(out.ipv4_ihl)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_ihl, o1, (uint8_t)((d[0] >> 24) & 0xFu));
+        if (want<GM, G_IPV4>(out.ipv4_diffserv)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_diffserv, o1, (uint8_t)((d[0] >> 16) & 0xFFu));
+        if (want<GM, G_IPV4>(out.ipv4_total_len)) st<(GM & G_NT) != 0, uint16_t>(out.ipv4_total_len, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_IPV4>(out.ipv4_identification)) st<(GM & G_NT) != 0, uint16_t>(out.ipv4_identification, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_IPV4>(out.ipv4_flags)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_flags, o1, (uint8_t)((d[1] >> 13) & 7u));
+        if (want<GM, G_IPV4>(out.ipv4_frag_startset)) st<(GM & G_NT) != 0, uint16_t>(out.ipv4_frag_startset, o2, (uint16_t)(d[1] & 0x1FFFu));
+        if (want<GM, G_IPV4>(out.ipv4_ttl)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_ttl, o1, (uint8_t)(d[2] >> 24));
+        if (want<GM, G_IPV4>(out.ipv4_protocol)) st<(GM & G_NT) != 0, uint8_t>(out.ipv4_protocol, o1, (uint8_t)((d[2] >> 16) & 0xFFu));
+        if (want<GM, G_IPV4>(out.ipv4_header_checksum)) st<(GM & G_NT) != 0, uint16_t>(out.ipv4_header_checksum, o2, (uint16_t)(d[2] & 0xFFFFu));
+        if (want<GM, G_IPV4>(out.ipv4_src)) st<(GM & G_NT) != 0, uint32_t>(out.ipv4_src, o4, d[3]);
+        if (want<GM, G_IPV4>(out.ipv4_dst)) st<(GM & G_NT) != 0, uint32_t>(out.ipv4_dst, o4, d[4]);
         if (want<GM, G_IPV4>(out.ipv4_csum_calc)) {
             // nine BE words, word 5 (byte offset 10) skipped; fold ((s>>16)+s)&0xFFFF (Q1)
             uint32_t s = (d[0] >> 16) + (d[0] & 0xFFFFu) + (d[1] >> 16) + (d[1] & 0xFFFFu) +
                          (d[2] >> 16) + (d[3] >> 16) + (d[3] & 0xFFFFu) + (d[4] >> 16) + (d[4] & 0xFFFFu);
             s = ((s >> 16) + s) & 0xFFFFu;
-            st<uint16_t>(out.ipv4_csum_calc, o2, h ? (uint16_t)(~s) : (uint16_t)0);
+            st<(GM & G_NT) != 0, uint16_t>(out.ipv4_csum_calc, o2, h ? (uint16_t)(~s) : (uint16_t)0);
         }
     }
     // IPv6 (headers.rs:577-592); src/dst as the raw 16 bytes of bytes(msb, lsb)
@@ -108,17 +111,17 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         want<GM, G_IPV6>(out.ipv6_src) || want<GM, G_IPV6>(out.ipv6_dst)) {
         uint32_t d[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         if (ok && r.f_ipv6 >= 0) pv.template hdr<10>((uint32_t)r.f_ipv6, 40, d);
-        if (want<GM, G_IPV6>(out.ipv6_version)) st<uint8_t>(out.ipv6_version, o1, (uint8_t)(d[0] >> 28));
-        if (want<GM, G_IPV6>(out.ipv6_traffic_class)) st<uint8_t>(out.ipv6_traffic_class, o1, (uint8_t)((d[0] >> 20) & 0xFFu));
-        if (want<GM, G_IPV6>(out.ipv6_flow_label)) st<uint32_t>(out.ipv6_flow_label, o4, d[0] & 0xFFFFFu);
-        if (want<GM, G_IPV6>(out.ipv6_payload_len)) st<uint16_t>(out.ipv6_payload_len, o2, (uint16_t)(d[1] >> 16));
-        if (want<GM, G_IPV6>(out.ipv6_next_hdr)) st<uint8_t>(out.ipv6_next_hdr, o1, (uint8_t)((d[1] >> 8) & 0xFFu));
-        if (want<GM, G_IPV6>(out.ipv6_hop_limit)) st<uint8_t>(out.ipv6_hop_limit, o1, (uint8_t)(d[1] & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_version)) st<(GM & G_NT) != 0, uint8_t>(out.ipv6_version, o1, (uint8_t)(d[0] >> 28));
+        if (want<GM, G_IPV6>(out.ipv6_traffic_class)) st<(GM & G_NT) != 0, uint8_t>(out.ipv6_traffic_class, o1, (uint8_t)((d[0] >> 20) & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_flow_label)) st<(GM & G_NT) != 0, uint32_t>(out.ipv6_flow_label, o4, d[0] & 0xFFFFFu);
+        if (want<GM, G_IPV6>(out.ipv6_payload_len)) st<(GM & G_NT) != 0, uint16_t>(out.ipv6_payload_len, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_IPV6>(out.ipv6_next_hdr)) st<(GM & G_NT) != 0, uint8_t>(out.ipv6_next_hdr, o1, (uint8_t)((d[1] >> 8) & 0xFFu));
+        if (want<GM, G_IPV6>(out.ipv6_hop_limit)) st<(GM & G_NT) != 0, uint8_t>(out.ipv6_hop_limit, o1, (uint8_t)(d[1] & 0xFFu));
         if (want<GM, G_IPV6>(out.ipv6_src))
-            st<uint4>(reinterpret_cast<uint4*>(out.ipv6_src), o16,
+            st<(GM & G_NT) != 0, uint4>(reinterpret_cast<uint4*>(out.ipv6_src), o16,
                       make_uint4(bswap32(d[2]), bswap32(d[3]), bswap32(d[4]), bswap32(d[5])));
         if (want<GM, G_IPV6>(out.ipv6_dst))
-            st<uint4>(reinterpret_cast<uint4*>(out.ipv6_dst), o16,
+            st<(GM & G_NT) != 0, uint4>(reinterpret_cast<uint4*>(out.ipv6_dst), o16,
                       make_uint4(bswap32(d[6]), bswap32(d[7]), bswap32(d[8]), bswap32(d[9])));
     }
     // TCP (headers.rs:606-622)
@@ -128,26 +131,26 @@ __device__ __forceinline__ void emit_fields(const pkt_out_t& out, uint32_t i, co
         want<GM, G_TCP>(out.tcp_urgent_ptr)) {
         uint32_t d[5] = {0, 0, 0, 0, 0};
         if (ok && r.f_tcp >= 0) pv.template hdr<5>((uint32_t)r.f_tcp, 20, d);
-        if (want<GM, G_TCP>(out.tcp_src)) st<uint16_t>(out.tcp_src, o2, (uint16_t)(d[0] >> 16));
-        if (want<GM, G_TCP>(out.tcp_dst)) st<uint16_t>(out.tcp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
-        if (want<GM, G_TCP>(out.tcp_seq_no)) st<uint32_t>(out.tcp_seq_no, o4, d[1]);
-        if (want<GM, G_TCP>(out.tcp_ack_no)) st<uint32_t>(out.tcp_ack_no, o4, d[2]);
-        if (want<GM, G_TCP>(out.tcp_data_startset)) st<uint8_t>(out.tcp_data_startset, o1, (uint8_t)(d[3] >> 28));
-        if (want<GM, G_TCP>(out.tcp_res)) st<uint8_t>(out.tcp_res, o1, (uint8_t)((d[3] >> 24) & 0xFu));
-        if (want<GM, G_TCP>(out.tcp_flags)) st<uint8_t>(out.tcp_flags, o1, (uint8_t)((d[3] >> 16) & 0xFFu));
-        if (want<GM, G_TCP>(out.tcp_window)) st<uint16_t>(out.tcp_window, o2, (uint16_t)(d[3] & 0xFFFFu));
-        if (want<GM, G_TCP>(out.tcp_checksum)) st<uint16_t>(out.tcp_checksum, o2, (uint16_t)(d[4] >> 16));
-        if (want<GM, G_TCP>(out.tcp_urgent_ptr)) st<uint16_t>(out.tcp_urgent_ptr, o2, (uint16_t)(d[4] & 0xFFFFu));
+        if (want<GM, G_TCP>(out.tcp_src)) st<(GM & G_NT) != 0, uint16_t>(out.tcp_src, o2, (uint16_t)(d[0] >> 16));
+        if (want<GM, G_TCP>(out.tcp_dst)) st<(GM & G_NT) != 0, uint16_t>(out.tcp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_TCP>(out.tcp_seq_no)) st<(GM & G_NT) != 0, uint32_t>(out.tcp_seq_no, o4, d[1]);
+        if (want<GM, G_TCP>(out.tcp_ack_no)) st<(GM & G_NT) != 0, uint32_t>(out.tcp_ack_no, o4, d[2]);
+        if (want<GM, G_TCP>(out.tcp_data_startset)) st<(GM & G_NT) != 0, uint8_t>(out.tcp_data_startset, o1, (uint8_t)(d[3] >> 28));
+        if (want<GM, G_TCP>(out.tcp_res)) st<(GM & G_NT) != 0, uint8_t>(out.tcp_res, o1, (uint8_t)((d[3] >> 24) & 0xFu));
+        if (want<GM, G_TCP>(out.tcp_flags)) st<(GM & G_NT) != 0, uint8_t>(out.tcp_flags, o1, (uint8_t)((d[3] >> 16) & 0xFFu));
+        if (want<GM, G_TCP>(out.tcp_window)) st<(GM & G_NT) != 0, uint16_t>(out.tcp_window, o2, (uint16_t)(d[3] & 0xFFFFu));
+        if (want<GM, G_TCP>(out.tcp_checksum)) st<(GM & G_NT) != 0, uint16_t>(out.tcp_checksum, o2, (uint16_t)(d[4] >> 16));
+        if (want<GM, G_TCP>(out.tcp_urgent_ptr)) st<(GM & G_NT) != 0, uint16_t>(out.tcp_urgent_ptr, o2, (uint16_t)(d[4] & 0xFFFFu));
     }
     // UDP (headers.rs:625-634)
     if (want<GM, G_UDP>(out.udp_src) || want<GM, G_UDP>(out.udp_dst) || want<GM, G_UDP>(out.udp_length) ||
         want<GM, G_UDP>(out.udp_checksum)) {
         uint32_t d[2] = {0, 0};
         if (ok && r.f_udp >= 0) pv.template hdr<2>((uint32_t)r.f_udp, 8, d);
-        if (want<GM, G_UDP>(out.udp_src)) st<uint16_t>(out.udp_src, o2, (uint16_t)(d[0] >> 16));
-        if (want<GM, G_UDP>(out.udp_dst)) st<uint16_t>(out.udp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
-        if (want<GM, G_UDP>(out.udp_length)) st<uint16_t>(out.udp_length, o2, (uint16_t)(d[1] >> 16));
-        if (want<GM, G_UDP>(out.udp_checksum)) st<uint16_t>(out.udp_checksum, o2, (uint16_t)(d[1] & 0xFFFFu));
+        if (want<GM, G_UDP>(out.udp_src)) st<(GM & G_NT) != 0, uint16_t>(out.udp_src, o2, (uint16_t)(d[0] >> 16));
+        if (want<GM, G_UDP>(out.udp_dst)) st<(GM & G_NT) != 0, uint16_t>(out.udp_dst, o2, (uint16_t)(d[0] & 0xFFFFu));
+        if (want<GM, G_UDP>(out.udp_length)) st<(GM & G_NT) != 0, uint16_t>(out.udp_length, o2, (uint16_t)(d[1] >> 16));
+        if (want<GM, G_UDP>(out.udp_checksum)) st<(GM & G_NT) != 0, uint16_t>(out.udp_checksum, o2, (uint16_t)(d[1] & 0xFFFFu));
     }
 }
 
@@ -197,11 +200,11 @@ __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, 
 template <uint32_t GM>
 __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uint32_t len, const WalkResult& r) {
     const bool ok = r.status == PKT_OK;
-    if (want<GM, G_CHAIN>(out.status)) st<uint8_t>(out.status, i, (uint8_t)r.status);
-    if (want<GM, G_CHAIN>(out.n_hdrs)) st<uint8_t>(out.n_hdrs, i, ok ? (uint8_t)r.n : (uint8_t)0);
-    if (want<GM, G_CHAIN>(out.payload_off)) st<uint16_t>(out.payload_off, 2 * i, ok ? (uint16_t)r.payload_off : (uint16_t)0);
-    if (want<GM, G_CHAIN>(out.payload_len)) st<uint16_t>(out.payload_len, 2 * i, ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0);
-    if (want<GM, G_CHAIN>(out.hdr_mask)) st<uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
+    if (want<GM, G_CHAIN>(out.status)) st<(GM & G_NT) != 0, uint8_t>(out.status, i, (uint8_t)r.status);
+    if (want<GM, G_CHAIN>(out.n_hdrs)) st<(GM & G_NT) != 0, uint8_t>(out.n_hdrs, i, ok ? (uint8_t)r.n : (uint8_t)0);
+    if (want<GM, G_CHAIN>(out.payload_off)) st<(GM & G_NT) != 0, uint16_t>(out.payload_off, 2 * i, ok ? (uint16_t)r.payload_off : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.payload_len)) st<(GM & G_NT) != 0, uint16_t>(out.payload_len, 2 * i, ok ? (uint16_t)(len - r.payload_off) : (uint16_t)0);
+    if (want<GM, G_CHAIN>(out.hdr_mask)) st<(GM & G_NT) != 0, uint32_t>(out.hdr_mask, 4 * i, ok ? r.mask : 0u);
 }
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -562,11 +565,11 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
 hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s) {
-    if (wk == 1) {
+    if (wk == 1) {  // indexed batches: non-temporal column stores
         switch (gm) {
-            case G_CHAIN: return launch_mode<NCH, G_CHAIN, 1>(kp, mode, s);
-            case G_ALL: return launch_mode<NCH, G_ALL, 1>(kp, mode, s);
-            default: return launch_mode<NCH, G_RUNTIME, 1>(kp, mode, s);
+            case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s);
+            case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s);
+            default: return launch_mode<NCH, G_RUNTIME | G_NT, 1>(kp, mode, s);
         }
     }
     switch (gm) {
