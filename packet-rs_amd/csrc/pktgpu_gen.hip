@@ -41,6 +41,11 @@ using pktgpu::put_bits;
 
 namespace {
 
+#ifndef PKTGPU_GEN_NT
+// non-temporal stores of the generated packets (region kernel): value arrays 58.7 -> 46.1 us, new
+// packets 42.9 -> 41.5 us (profiles/ab/r02nt2_nt_wide_stores.txt)
+#define PKTGPU_GEN_NT 1
+#endif
 constexpr int kMaxGenFields = 32;
 constexpr int kMaxGenCsum = 8;
 constexpr uint32_t kGenBlock = 256;
@@ -228,7 +233,13 @@ __global__ __launch_bounds__(64) void gen_region_kernel(GenParams p) {
     for (uint32_t o = lane * 16u; o < bytes; o += 1024u) {
         const uint32_t q = o >> 4, pk = (q * p.pk_magic) >> 20, k = q - pk * p.ppp;
         const int32_t sk = sl[k];
-        *reinterpret_cast<uint4*>(d + o) = sk >= 0 ? *reinterpret_cast<const uint4*>(region + (pk * p.nd + (uint32_t)sk) * 16u) : tp[k];
+        const uint4 v = sk >= 0 ? *reinterpret_cast<const uint4*>(region + (pk * p.nd + (uint32_t)sk) * 16u) : tp[k];
+#if PKTGPU_GEN_NT
+        typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+        __builtin_nontemporal_store(v4u{v.x, v.y, v.z, v.w}, reinterpret_cast<v4u*>(d + o));
+#else
+        *reinterpret_cast<uint4*>(d + o) = v;
+#endif
     }
 }
 }  // namespace

@@ -393,6 +393,14 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    // A wave whose 64 outputs lie back to back in the destination (a fixed-stride slab of whole
+    // slots, or packed outputs) stores its whole chunks non-temporally: C2 33.7 -> 30.8 us, C4
+    // packed 119 -> 102 us; with gaps between the outputs (a pcap's record headers left untouched)
+    // the partial edge chunks share those lines and plain stores are faster (142 vs 147 us)
+    // (profiles/ab/r02nt2_nt_wide_stores.txt).
+    const uint64_t nd_ = __shfl_down(dst, 1u, 64);
+    const bool nflat = __shfl_down((int)flat, 1u, 64) != 0;
+    const bool dense = __ballot(lane == 63 || (flat && nflat && dst + len == nd_)) == ~0ull;
     // One chunk per lane per round, software-pipelined by one round: the next round's load is
     // issued before this round's store (a store may alias the next chunk's source, so the
     // compiler keeps load -> store -> load otherwise: one memory round trip per round).  (Issuing
@@ -410,7 +418,12 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     };
     auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4]) {
         if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
-            *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(o[0], o[1], o[2], o[3]);
+            if (dense) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(p.dst + ca));
+            } else {
+                *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(o[0], o[1], o[2], o[3]);
+            }
         } else {
             store_edge_chunk(p.dst, p.dst_len, ca, o, lo, hi);
         }
