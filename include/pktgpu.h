@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PKTGPU_ABI_VERSION 3
+#define PKTGPU_ABI_VERSION 4
 
 /* Maximum number of headers recorded per packet.  The reference recursion is unbounded
  * (fast.rs:53 VLAN stacks, :69 MPLS stacks, :89/:92/:104/:107 IP-in-IP, :168/:186/:219
@@ -330,8 +330,9 @@ int pkt_set_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *
 
 /* pkt_set_fields followed, in the same launch, by pkt_ipv4_update_checksum of the
  * `ipv4_occurrence`-th IPv4 header (< 0: no checksum refresh; nspec may then be 0 for a refresh
- * alone): the header rewrite of the update+clone loop (tests/lib.rs:778-787: setters, then
- * utils.rs:233-236's checksum) as one pass over each packet's bytes. */
+ * alone), as one pass over each packet's bytes.  The reference's update+clone loop
+ * (tests/lib.rs:778-787) is setters only (set_etype; ipv4_occurrence < 0); the checksum refresh is
+ * what the create_* builders do after setting IPv4 fields (utils.rs:233-236). */
 int pkt_set_fields_csum(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain_t *chain,
                         const pkt_field_spec_t *specs, uint32_t nspec, const uint64_t *const *values,
                         int32_t ipv4_occurrence, void *stream);
@@ -420,11 +421,19 @@ int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint
 /* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
 uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
 
+/* The largest n_hdrs[i] over n packets (`n_hdrs`: a device column from pkt_parse_batch): the slot
+ * rows of hdr_type / hdr_off that hold data — a PacketSlice holds exactly its headers (lib.rs:136-140),
+ * so a copy or gather of a batch's chain moves rows [0, *max_out) only.  Blocking (waits for
+ * `stream`).  One such call at a time per ctx. */
+int pkt_chain_max_hdrs(pkt_ctx_t *ctx, const uint8_t *n_hdrs, uint64_t n, uint32_t *max_out, void *stream);
+
 /* ---- packed output buffers (host only, no device needed) ----
  * A column mask selects pkt_out_t members: bit k = the k-th pointer of pkt_out_t (0 = status,
  * ..., 48 = udp_checksum).  The packed layout puts every selected column of an n-packet output in
- * one buffer, in pkt_out_t order, each column starting on a 256-byte boundary (slot columns are
- * [PKT_MAX_HDRS][n]).  One buffer per shard is what the multi-GPU gather moves in one message. */
+ * one buffer, each column starting on a 256-byte boundary: the per-packet columns in pkt_out_t
+ * order, then the slot columns hdr_type and hdr_off ([PKT_MAX_HDRS][n] each) last.  One buffer per
+ * shard is what the multi-GPU gather moves; with only the used slot rows (pkt_out_packed_pieces)
+ * that is at most two contiguous pieces. */
 #define PKT_COL(k)      (1ull << (k))
 #define PKT_COLS_ALL    ((1ull << 49) - 1)
 #define PKT_COLS_CHAIN  0x7Full               /* status .. hdr_mask */
@@ -437,6 +446,12 @@ uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
 /* Fills `out` with the selected columns' pointers inside `base` (NULL columns elsewhere; `base`
  * may be NULL to size only) and sets *bytes to the buffer size. */
 int pkt_out_packed(uint64_t col_mask, uint64_t n, void *base, pkt_out_t *out, uint64_t *bytes);
+/* The byte ranges of an n-packet packed buffer that hold every selected column with only the first
+ * `rows` (<= PKT_MAX_HDRS) slot rows of hdr_type / hdr_off: piece k = [off[k], off[k] + len[k]),
+ * k < *npieces (2 when both slot columns are selected: the head through hdr_type's used rows, then
+ * hdr_off's used rows; else 1).  C2's chain + Ether/IPv4/UDP at rows = 3 is 69 B per packet. */
+int pkt_out_packed_pieces(uint64_t col_mask, uint64_t n, uint32_t rows, uint64_t off[2], uint64_t len[2],
+                          int *npieces);
 /* The column mask of a pkt_out_t (bit k set iff its k-th pointer is non-NULL). */
 uint64_t pkt_out_mask(const pkt_out_t *out);
 /* [lo, hi) of shard i of n packets split into `nshards` contiguous blocks whose sizes differ by
@@ -456,6 +471,7 @@ typedef struct pkt_mgpu pkt_mgpu_t;
 int         pkt_mgpu_create(const int *devices, int ndev, pkt_mgpu_t **mg);
 int         pkt_mgpu_destroy(pkt_mgpu_t *mg);
 int         pkt_mgpu_ndev(const pkt_mgpu_t *mg);
+/* The handle's last error; pkt_mgpu_last_error(NULL) = why this thread's last pkt_mgpu_create failed. */
 const char *pkt_mgpu_last_error(const pkt_mgpu_t *mg);
 /* The per-device ctx (tuning knobs, other batched calls) and work stream (a hipStream_t). */
 pkt_ctx_t  *pkt_mgpu_ctx(pkt_mgpu_t *mg, int shard);
@@ -470,7 +486,9 @@ int pkt_mgpu_parse(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64
 int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uint64_t *bytes,
                     void *recv, uint64_t recv_len, const uint64_t *recv_off);
 /* pkt_mgpu_parse, then the gather of every shard's packed tuple buffer into `recv` on the root
- * (consecutive 256-B aligned blocks).  root_views (host array of ndev pkt_out_t, may be NULL)
+ * (consecutive 256-B aligned blocks, each laid out as that shard's packed buffer).  Only the used
+ * slot rows move (pkt_chain_max_hdrs of each shard when n_hdrs is among the columns, so the call
+ * waits for the parses before it queues the gather; all 16 rows otherwise).  root_views (host array of ndev pkt_out_t, may be NULL)
  * receives the column pointers of each shard's tuples inside `recv`.  With `merge` = 1 the
  * tuples land as ONE packed output of sum(n) packets instead (recv = pkt_out_packed(col_mask,
  * sum n) bytes, shards in order: what pkt_parse_batch over the whole batch would write); the

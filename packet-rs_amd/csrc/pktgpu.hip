@@ -641,9 +641,70 @@ hipError_t grow(T* (&buf)[HostPipe::kSlots], uint64_t& cap, uint64_t need) {
 }
 
 
+// The largest n_hdrs of a batch: how many slot rows of hdr_type / hdr_off hold data.  16 bytes per
+// thread (grid-strided), a wave max, one atomicMax per wave that saw a non-zero count.
+__global__ __launch_bounds__(256) void max_hdrs_kernel(const uint8_t* nh, uint64_t n, uint32_t* out) {
+    uint32_t m = 0;
+    const uint64_t step = (uint64_t)gridDim.x * 256u * 16u;
+    const bool al = ((uintptr_t)nh & 15) == 0;
+    for (uint64_t i = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 16u; i < n; i += step) {
+        if (al && i + 16 <= n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(nh + i);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                m = max(max(m, w[k] >> 24), max(max(w[k] & 0xFFu, (w[k] >> 8) & 0xFFu), (w[k] >> 16) & 0xFFu));
+        } else {
+            for (uint64_t k = i; k < i + 16 && k < n; k++) m = max(m, (uint32_t)nh[k]);
+        }
+    }
+#pragma unroll
+    for (int sft = 32; sft >= 1; sft >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, sft, 64));
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+}
+
+hipError_t ensure_max_scratch(pkt_ctx* ctx) {
+    if (ctx->mx.dev) return hipSuccess;
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->mx.dev), MaxScratch::kWords * sizeof(uint32_t));
+    if (e == hipSuccess)
+        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->mx.host), MaxScratch::kWords * sizeof(uint32_t),
+                          hipHostMallocDefault);
+    if (e != hipSuccess) {
+        (void)hipFree(ctx->mx.dev);
+        ctx->mx.dev = nullptr;
+        ctx->mx.host = nullptr;
+    }
+    return e;
+}
+
+// Queue the reduction of n_hdrs[0, n) into scratch word `w` and its copy to the host mirror on `s`.
+hipError_t max_hdrs_async(pkt_ctx* ctx, const uint8_t* nh, uint64_t n, int w, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(ctx->mx.dev + w, 0, sizeof(uint32_t), s);
+    if (e != hipSuccess) return e;
+    if (n) {
+        const unsigned grid = (unsigned)std::min<uint64_t>((n + 4095) / 4096, 1024);
+        hipLaunchKernelGGL(max_hdrs_kernel, dim3(grid), dim3(256), 0, s, nh, n, ctx->mx.dev + w);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipMemcpyAsync(ctx->mx.host + w, ctx->mx.dev + w, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+}
+
 }  // namespace
 
 extern "C" {
+
+int pkt_chain_max_hdrs(pkt_ctx_t* ctx, const uint8_t* n_hdrs, uint64_t n, uint32_t* max_out, void* stream) {
+    if (!ctx || !max_out || (n && !n_hdrs)) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = ensure_max_scratch(ctx);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pkt_chain_max_hdrs scratch");
+    const int w = MaxScratch::kWords - 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if ((e = max_hdrs_async(ctx, n_hdrs, n, w, s)) != hipSuccess) return hip_fail(ctx, e, "max_hdrs_kernel");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+    *max_out = std::min<uint32_t>(ctx->mx.host[w], PKT_MAX_HDRS);
+    return PKT_SUCCESS;
+}
 
 int pkt_ctx_create(int device, pkt_ctx_t** out) {
     if (!out) return PKT_ERR_INVALID_ARG;
@@ -662,6 +723,12 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
 }
 
 int pkt_ctx_destroy(pkt_ctx_t* ctx) {
+    if (ctx && ctx->mx.dev) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->mx.dev);
+        (void)hipHostFree(ctx->mx.host);
+    }
     if (ctx && (ctx->pc.buf || ctx->pc.ctl)) {
         (void)hipSetDevice(ctx->device);
         (void)hipDeviceSynchronize();
@@ -673,6 +740,7 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         for (int k = 0; k < HostPipe::kSlots; k++) {
             (void)hipStreamSynchronize(ctx->hp.s[k]);
             (void)hipStreamDestroy(ctx->hp.s[k]);
+            if (ctx->hp.ev[k]) (void)hipEventDestroy(ctx->hp.ev[k]);
             (void)hipFree(ctx->hp.slab[k]);
             (void)hipFree(ctx->hp.offs[k]);
             (void)hipFree(ctx->hp.lens[k]);
@@ -813,6 +881,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     if (!hp.init) {
         for (int k = 0; k < HostPipe::kSlots; k++) {
             e = hipStreamCreateWithFlags(&hp.s[k], hipStreamNonBlocking);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&hp.ev[k], hipEventDisableTiming);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamCreate");
         }
         hp.init = true;
@@ -886,6 +955,29 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         hp.pkt_cap = std::min(cap8, cap4);
     }
 
+    // Slot rows move only as far as each chunk's largest n_hdrs (when n_hdrs is requested): the
+    // chunk's count is reduced on the device after its parse and read on the host one chunk later,
+    // so the host waits for chunk k-1 only after chunk k is queued.
+    const bool slot_rows = (hcol[kColHdrType] || hcol[kColHdrOff]) && hcol[1] != nullptr;
+    if (slot_rows && (e = ensure_max_scratch(ctx)) != hipSuccess) return hip_fail(ctx, e, "max scratch");
+    auto copy_slots = [&](uint64_t kk) -> hipError_t {  // chunk kk's slot rows [0, R) to the host
+        const int q = (int)(kk % HostPipe::kSlots);
+        const uint64_t lo = kk * cn, m = std::min(n, lo + cn) - lo;
+        uint32_t rows = PKT_MAX_HDRS;
+        if (slot_rows) {
+            hipError_t es = hipEventSynchronize(hp.ev[q]);
+            if (es != hipSuccess) return es;
+            rows = std::min<uint32_t>(ctx->mx.host[q], PKT_MAX_HDRS);
+        }
+        for (int c : {kColHdrType, kColHdrOff}) {
+            if (!hcol[c] || !rows) continue;
+            const uint64_t sz = kColSize[c];
+            hipError_t es = hipMemcpy2DAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, n * sz, hp.out[q] + col_off[c],
+                                             m * sz, m * sz, rows, hipMemcpyDeviceToHost, hp.s[q]);
+            if (es != hipSuccess) return es;
+        }
+        return hipSuccess;
+    };
     int rc = PKT_SUCCESS;
     for (uint64_t k = 0; k < nchunks && rc == PKT_SUCCESS; k++) {
         const int q = (int)(k % HostPipe::kSlots);
@@ -916,17 +1008,22 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         // (the device buffer always has >= 16 readable bytes, so a view shorter than 16 is safe)
         rc = parse_impl(ctx, &db, entry, &dout, s, b->offsets ? base : 0, ctx->staging);
         if (rc != PKT_SUCCESS) break;
-        // out: every requested column into its host rows [lo, hi)
+        // out: every requested per-packet column into its host rows [lo, hi); the slot rows of this
+        // chunk once its count is known (after the next chunk is queued)
         for (int c = 0; c < 49 && e == hipSuccess; c++) {
-            if (!hcol[c]) continue;
-            uint8_t* h = const_cast<uint8_t*>(hcol[c]);
+            if (!hcol[c] || c == kColHdrType || c == kColHdrOff) continue;
             const uint64_t sz = kColSize[c];
-            if (c == kColHdrType || c == kColHdrOff)
-                e = hipMemcpy2DAsync(h + lo * sz, n * sz, dcol[c], m * sz, m * sz, PKT_MAX_HDRS,
-                                     hipMemcpyDeviceToHost, s);
-            else
-                e = hipMemcpyAsync(h + lo * sz, dcol[c], m * sz, hipMemcpyDeviceToHost, s);
+            e = hipMemcpyAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, dcol[c], m * sz, hipMemcpyDeviceToHost, s);
         }
+        if (e == hipSuccess && slot_rows) {
+            e = max_hdrs_async(ctx, dcol[1], m, q, s);
+            if (e == hipSuccess) e = hipEventRecord(hp.ev[q], s);
+        }
+        if (e == hipSuccess && k > 0) e = copy_slots(k - 1);
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMemcpyAsync D2H");
+    }
+    if (rc == PKT_SUCCESS && nchunks > 0) {
+        e = copy_slots(nchunks - 1);
         if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMemcpyAsync D2H");
     }
     for (int k = 0; k < HostPipe::kSlots; k++) {

@@ -13,6 +13,7 @@ struct HostPipe {
     static constexpr int kSlots = 3;
     bool init = false;
     hipStream_t s[kSlots] = {};
+    hipEvent_t ev[kSlots] = {};  // a slot's slot-row count has reached the host (pkt_chain_max_hdrs words)
     uint8_t* slab[kSlots] = {};
     uint64_t* offs[kSlots] = {};
     uint32_t* lens[kSlots] = {};
@@ -41,10 +42,19 @@ inline uint64_t col_bytes(int c, uint64_t n) {
     return n * kColSize[c] * ((c == kColHdrType || c == kColHdrOff) ? PKT_MAX_HDRS : 1);
 }
 
+// Words of the slot-row reduction (pkt_chain_max_hdrs): one per host-pipeline slot + one for the
+// blocking call, on the device and mirrored in pinned host memory.
+struct MaxScratch {
+    static constexpr int kWords = HostPipe::kSlots + 1;
+    uint32_t* dev = nullptr;
+    uint32_t* host = nullptr;
+};
+
 struct pkt_ctx {
     int device;
     HostPipe hp;
     PcapScratch pc;
+    MaxScratch mx;
     uint32_t window;  // 0 = auto
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)

@@ -28,6 +28,13 @@ struct pkt_mgpu {
 namespace {
 
 constexpr uint64_t kAlign = 256;
+// Why the last pkt_mgpu_create on this thread failed (there is no handle to hold it):
+// pkt_mgpu_last_error(NULL) returns it.
+thread_local std::string g_create_err;
+int create_fail(int code, const std::string& msg) {
+    g_create_err = msg;
+    return code;
+}
 inline uint64_t round_up(uint64_t x) { return (x + kAlign - 1) & ~(kAlign - 1); }
 
 int mfail(pkt_mgpu* mg, int code, const std::string& msg) {
@@ -41,15 +48,45 @@ int mnccl(pkt_mgpu* mg, ncclResult_t r, const char* what) {
     return mfail(mg, PKT_ERR_HIP, std::string(what) + ": " + ncclGetErrorString(r));
 }
 
-// Offset of column c inside a packed buffer of n packets (selected columns only, in order).
+// Offset of column c inside a packed buffer of n packets: the selected per-packet columns in
+// pkt_out_t order, then the slot columns hdr_type and hdr_off ([PKT_MAX_HDRS][n] each) last, so
+// that a batch's used slot rows [0, rows) end the first piece of the buffer (packed_pieces).
 uint64_t packed_layout(uint64_t mask, uint64_t n, uint64_t* off /* [kNumCols] or NULL */) {
     uint64_t o = 0;
-    for (int c = 0; c < kNumCols; c++) {
-        if (!(mask >> c & 1)) continue;
+    auto place = [&](int c) {
+        if (!(mask >> c & 1)) return;
         if (off) off[c] = o;
         o += round_up(col_bytes(c, n));
-    }
+    };
+    for (int c = 0; c < kNumCols; c++)
+        if (c != kColHdrType && c != kColHdrOff) place(c);
+    place(kColHdrType);
+    place(kColHdrOff);
     return o;
+}
+
+// The byte ranges of an n-packet packed buffer that hold every selected column with only the
+// first `rows` slot rows (a PacketSlice holds exactly its headers, lib.rs:136-140): the head up to
+// the end of hdr_type's used rows (or of hdr_off's when hdr_type is not selected), then hdr_off's
+// used rows.  Returns the number of pieces (1 or 2).
+int packed_pieces(uint64_t mask, uint64_t n, uint32_t rows, uint64_t off[2], uint64_t len[2]) {
+    uint64_t co[kNumCols];
+    const uint64_t total = packed_layout(mask, n, co);
+    const bool t = mask >> kColHdrType & 1, h = mask >> kColHdrOff & 1;
+    off[0] = off[1] = len[1] = 0;
+    if (!t && !h) {
+        len[0] = total;
+        return 1;
+    }
+    if (t) {
+        len[0] = co[kColHdrType] + (uint64_t)rows * n * kColSize[kColHdrType];
+        if (!h) return 1;
+        off[1] = co[kColHdrOff];
+        len[1] = (uint64_t)rows * n * kColSize[kColHdrOff];
+        return len[1] ? 2 : 1;
+    }
+    len[0] = co[kColHdrOff] + (uint64_t)rows * n * kColSize[kColHdrOff];
+    return 1;
 }
 
 // Merged gather plan: (source offset in the shard buffer, destination offset in the root
@@ -57,7 +94,8 @@ uint64_t packed_layout(uint64_t mask, uint64_t n, uint64_t* off /* [kNumCols] or
 struct Piece {
     uint64_t src, dst, bytes;
 };
-void merged_pieces(uint64_t mask, uint64_t n_i, uint64_t lo, uint64_t n_total, std::vector<Piece>& out) {
+void merged_pieces(uint64_t mask, uint64_t n_i, uint64_t lo, uint64_t n_total, uint32_t rows,
+                   std::vector<Piece>& out) {
     uint64_t so[kNumCols], dof[kNumCols];
     packed_layout(mask, n_i, so);
     packed_layout(mask, n_total, dof);
@@ -67,7 +105,7 @@ void merged_pieces(uint64_t mask, uint64_t n_i, uint64_t lo, uint64_t n_total, s
         if (!(mask >> c & 1)) continue;
         const uint64_t esz = kColSize[c];
         if (c == kColHdrType || c == kColHdrOff) {
-            for (uint64_t j = 0; j < PKT_MAX_HDRS; j++)
+            for (uint64_t j = 0; j < rows; j++)
                 out.push_back({so[c] + j * n_i * esz, dof[c] + (j * n_total + lo) * esz, n_i * esz});
         } else {
             out.push_back({so[c], dof[c] + lo * esz, n_i * esz});
@@ -92,6 +130,12 @@ int pkt_out_packed(uint64_t mask, uint64_t n, void* base, pkt_out_t* out, uint64
     return PKT_SUCCESS;
 }
 
+int pkt_out_packed_pieces(uint64_t mask, uint64_t n, uint32_t rows, uint64_t* off, uint64_t* len, int* npieces) {
+    if (mask >> kNumCols || rows > PKT_MAX_HDRS || !off || !len || !npieces) return PKT_ERR_INVALID_ARG;
+    *npieces = packed_pieces(mask, n, rows, off, len);
+    return PKT_SUCCESS;
+}
+
 uint64_t pkt_out_mask(const pkt_out_t* out) {
     if (!out) return 0;
     const void* const* cols = reinterpret_cast<const void* const*>(out);
@@ -110,14 +154,18 @@ int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t* lo, uint64_t* hi) 
 }
 
 int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
-    if (!out || !devices || ndev <= 0) return PKT_ERR_INVALID_ARG;
+    g_create_err.clear();
+    if (!out || !devices || ndev <= 0) return create_fail(PKT_ERR_INVALID_ARG, "null argument or ndev <= 0");
     *out = nullptr;
     int count = 0;
-    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return PKT_ERR_NO_DEVICE;
+    if (hipGetDeviceCount(&count) != hipSuccess || count == 0) return create_fail(PKT_ERR_NO_DEVICE, "no HIP device");
     for (int i = 0; i < ndev; i++) {
-        if (devices[i] < 0 || devices[i] >= count) return PKT_ERR_INVALID_ARG;
+        if (devices[i] < 0 || devices[i] >= count)
+            return create_fail(PKT_ERR_INVALID_ARG, "device " + std::to_string(devices[i]) + " of " +
+                                                        std::to_string(count) + " visible");
         for (int j = 0; j < i; j++)
-            if (devices[j] == devices[i]) return PKT_ERR_INVALID_ARG;  // one communicator per device
+            if (devices[j] == devices[i])  // one communicator per device
+                return create_fail(PKT_ERR_INVALID_ARG, "device " + std::to_string(devices[i]) + " listed twice");
     }
     pkt_mgpu* mg = new pkt_mgpu();
     mg->ndev = ndev;
@@ -126,23 +174,31 @@ int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
     mg->stream.assign(ndev, nullptr);
     mg->comm.assign(ndev, nullptr);
     int rc = PKT_SUCCESS;
+    std::string why;
     for (int i = 0; i < ndev && rc == PKT_SUCCESS; i++) {
         rc = pkt_ctx_create(devices[i], &mg->ctx[i]);
-        if (rc != PKT_SUCCESS) break;
+        if (rc != PKT_SUCCESS) {
+            why = "pkt_ctx_create(" + std::to_string(devices[i]) + ") failed";
+            break;
+        }
         hipError_t e = hipSetDevice(devices[i]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&mg->stream[i], hipStreamNonBlocking);
-        if (e != hipSuccess) rc = PKT_ERR_HIP;
+        if (e != hipSuccess) {
+            rc = PKT_ERR_HIP;
+            why = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+        }
     }
     if (rc == PKT_SUCCESS) {
         ncclResult_t r = ncclCommInitAll(mg->comm.data(), ndev, mg->dev.data());
         if (r != ncclSuccess) {
             for (auto& c : mg->comm) c = nullptr;
             rc = PKT_ERR_HIP;
+            why = std::string("ncclCommInitAll: ") + ncclGetErrorString(r);
         }
     }
     if (rc != PKT_SUCCESS) {
         pkt_mgpu_destroy(mg);
-        return rc;
+        return create_fail(rc, why);
     }
     *out = mg;
     return PKT_SUCCESS;
@@ -162,7 +218,7 @@ int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
 }
 
 int pkt_mgpu_ndev(const pkt_mgpu_t* mg) { return mg ? mg->ndev : 0; }
-const char* pkt_mgpu_last_error(const pkt_mgpu_t* mg) { return mg ? mg->err.c_str() : "null handle"; }
+const char* pkt_mgpu_last_error(const pkt_mgpu_t* mg) { return mg ? mg->err.c_str() : g_create_err.c_str(); }
 pkt_ctx_t* pkt_mgpu_ctx(pkt_mgpu_t* mg, int i) { return (mg && i >= 0 && i < mg->ndev) ? mg->ctx[i] : nullptr; }
 void* pkt_mgpu_stream(pkt_mgpu_t* mg, int i) {
     return (mg && i >= 0 && i < mg->ndev) ? reinterpret_cast<void*>(mg->stream[i]) : nullptr;
@@ -215,34 +271,51 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
     if (!mg || !batches || !shard_out) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
     if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
     if (merge != 0 && merge != 1) return mfail(mg, PKT_ERR_INVALID_ARG, "bad merge flag");
+    const int nd = mg->ndev;
+    // validate the receive buffer before anything is launched or any view is filled in
+    uint64_t n_total = 0, need = 0;
+    for (int i = 0; i < nd; i++) {
+        n_total += batches[i].n;
+        need = round_up(need) + packed_layout(mask, batches[i].n, nullptr);
+    }
+    if (merge) need = packed_layout(mask, n_total, nullptr);
+    if (n_total && !recv) return mfail(mg, PKT_ERR_INVALID_ARG, "null recv");
+    if (need > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
     int rc = pkt_mgpu_parse(mg, batches, entry, mask, shard_out);
     if (rc != PKT_SUCCESS) return rc;
-    const int nd = mg->ndev;
-    if (!merge) {
-        std::vector<const void*> send(nd);
-        std::vector<uint64_t> bytes(nd), off(nd);
-        uint64_t o = 0;
+    // Slot rows to move per shard: its largest n_hdrs (rows past it hold nothing), found on the
+    // device after the parse (the shards' parses all run while the host waits for the first).
+    std::vector<uint32_t> rows(nd, PKT_MAX_HDRS);
+    if (mask >> 1 & 1) {  // n_hdrs is among the columns
         for (int i = 0; i < nd; i++) {
-            send[i] = shard_out[i];
-            bytes[i] = packed_layout(mask, batches[i].n, nullptr);
-            off[i] = o;
-            o = round_up(o + bytes[i]);
-            if (root_views) pkt_out_packed(mask, batches[i].n, static_cast<uint8_t*>(recv) + off[i], &root_views[i], nullptr);
+            if (!batches[i].n) continue;
+            pkt_out_t o;
+            pkt_out_packed(mask, batches[i].n, shard_out[i], &o, nullptr);
+            rc = pkt_chain_max_hdrs(mg->ctx[i], o.n_hdrs, batches[i].n, &rows[i], mg->stream[i]);
+            if (rc != PKT_SUCCESS)
+                return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
         }
-        return pkt_mgpu_gather(mg, root, send.data(), bytes.data(), recv, recv_len, off.data());
     }
-    uint64_t n_total = 0;
-    for (int i = 0; i < nd; i++) n_total += batches[i].n;
-    if (packed_layout(mask, n_total, nullptr) > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
-    if (n_total && !recv) return mfail(mg, PKT_ERR_INVALID_ARG, "null recv");
-    if (root_views) pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
     std::vector<Piece> pieces;
+    uint64_t lo = 0, o = 0;
+    if (merge && root_views) pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
-    uint64_t lo = 0;
     for (int i = 0; i < nd && r == ncclSuccess; i++) {
-        merged_pieces(mask, batches[i].n, lo, n_total, pieces);
-        lo += batches[i].n;
+        if (merge) {
+            // each column (each used slot row) of the shard at its place in the whole batch's output
+            merged_pieces(mask, batches[i].n, lo, n_total, rows[i], pieces);
+            lo += batches[i].n;
+        } else {
+            // the shard's packed buffer at the next 256-B boundary of recv, used slot rows only
+            pieces.clear();
+            if (root_views) pkt_out_packed(mask, batches[i].n, static_cast<uint8_t*>(recv) + o, &root_views[i], nullptr);
+            uint64_t po[2], pl[2];
+            const int np = packed_pieces(mask, batches[i].n, rows[i], po, pl);
+            for (int k = 0; k < np; k++)
+                if (pl[k] && batches[i].n) pieces.push_back({po[k], o + po[k], pl[k]});
+            o = round_up(o + packed_layout(mask, batches[i].n, nullptr));
+        }
         for (const Piece& p : pieces) {
             r = ncclSend(static_cast<const uint8_t*>(shard_out[i]) + p.src, p.bytes, ncclUint8, root, mg->comm[i],
                          mg->stream[i]);

@@ -81,6 +81,8 @@ class Parser:
             self._L.pkt_ctx_set_window(self._ctx, window)
 
     def close(self):
+        for g in self.__dict__.pop("_gen_udp_cache", {}).values():  # pktgen.gen_udp's generators
+            g.close()
         for p in getattr(self, "_pinned", []):
             self._L.pkt_host_free(self._ctx, p)
         self._pinned = []

@@ -99,6 +99,10 @@ SIGNATURES = {
     # packed outputs + multi-GPU (pkt_mgpu_*)
     "pkt_out_packed": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, _P, ctypes.POINTER(PktOut),
                                       ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_out_packed_pieces": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint32,
+                                             ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                             ctypes.POINTER(ctypes.c_int)]),
+    "pkt_chain_max_hdrs": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), _P]),
     "pkt_out_mask": (ctypes.c_uint64, [ctypes.POINTER(PktOut)]),
     "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),

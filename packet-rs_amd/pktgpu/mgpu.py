@@ -106,6 +106,38 @@ class MultiParser:
     def synchronize(self):
         self._check(self._L.pkt_mgpu_synchronize(self._mg), "pkt_mgpu_synchronize")
 
+    def streams(self):
+        """The handle's per-device work streams (pkt_mgpu_stream) as torch ExternalStreams."""
+        torch = _torch()
+        if getattr(self, "_ext", None) is None:
+            self._ext = [torch.cuda.ExternalStream(self._L.pkt_mgpu_stream(self._mg, i), device=d)
+                         for i, d in enumerate(self.torch_devices)]
+        return self._ext
+
+    def _after_torch(self):
+        """The library's streams are non-blocking streams of their own: make each wait for the work
+        torch has queued on that device (e.g. a Generator.run slab, a non_blocking copy)."""
+        torch = _torch()
+        for d, ext in zip(self.torch_devices, self.streams()):
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(d))
+            ext.wait_event(ev)
+
+    def _before_torch(self, tensors):
+        """Order torch's current streams after the library's work, and tell the caching allocator
+        that every tensor the library touched is in use on the library's stream (so it is not
+        reused while a kernel or RCCL still reads or writes it)."""
+        torch = _torch()
+        ext = self.streams()
+        for d, e in zip(self.torch_devices, ext):
+            ev = torch.cuda.Event()
+            ev.record(e)
+            torch.cuda.current_stream(d).wait_event(ev)
+        by_dev = {d: e for d, e in zip(self.torch_devices, ext)}
+        for t in tensors:
+            if t is not None and t.is_cuda and t.device in by_dev:
+                t.record_stream(by_dev[t.device])
+
     # ---------------------------------------------------------------- inputs
     def shard_fixed(self, slab, n, stride, lens=None):
         """Copy the contiguous shards of a host fixed-stride slab (numpy uint8) to the devices:
@@ -159,8 +191,10 @@ class MultiParser:
         if shard_out is None:
             shard_out = self.alloc_shard_outputs(shards, cols)
         ptrs = (ctypes.c_void_p * self.ndev)(*[b.data_ptr() for b in shard_out])
+        self._after_torch()
         self._check(self._L.pkt_mgpu_parse(self._mg, self._batches(shards), e, schema.column_mask(cols), ptrs),
                     "pkt_mgpu_parse")
+        self._before_torch(list(shard_out) + [t for sh in shards for t in (sh[0], sh[3], sh[4])])
         return shard_out
 
     def recv_bytes(self, shards, columns, merge):
@@ -173,7 +207,10 @@ class MultiParser:
                      shard_out=None, recv=None):
         """Parse + RCCL gather into one device buffer on devices[root].  Returns (views, recv,
         shard_out): views = one {column: tensor} for merge=True (the whole batch), else one per
-        shard.  Asynchronous on the handle's streams; call synchronize() before reading."""
+        shard.  Ordered like a torch op: the library's streams first wait for torch's current
+        streams, torch's current streams then wait for the gather, and every tensor involved is
+        marked in use on the library's streams (record_stream), so torch work may consume the
+        results right away; synchronize() is needed only before host reads."""
         torch = _torch()
         e = schema.ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
         cols = resolve_columns(columns)
@@ -185,9 +222,11 @@ class MultiParser:
             recv = torch.empty(max(1, need), dtype=torch.uint8, device=self.torch_devices[root])
         ptrs = (ctypes.c_void_p * self.ndev)(*[b.data_ptr() for b in shard_out])
         views = (self._lib.PktOut * self.ndev)()
+        self._after_torch()
         self._check(self._L.pkt_mgpu_parse_gather(self._mg, self._batches(shards), e, mask, ptrs, root,
                                                   ctypes.c_void_p(recv.data_ptr()), recv.numel(),
                                                   1 if merge else 0, views), "pkt_mgpu_parse_gather")
+        self._before_torch(list(shard_out) + [recv] + [t for sh in shards for t in (sh[0], sh[3], sh[4])])
         if merge:
             return packed_views(recv, cols, sum(s[1] for s in shards)), recv, shard_out
         out, o = [], 0

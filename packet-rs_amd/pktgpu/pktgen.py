@@ -111,11 +111,22 @@ class Generator:
         stride = stride or self.default_stride()
         if dst is None:
             dst = torch.empty(n * stride, dtype=torch.uint8, device=self.P.torch_device)
+        # pkt_gen_run takes no length for dst or the value arrays: check them here (not with
+        # assert, which python -O strips)
+        if not (isinstance(dst, torch.Tensor) and dst.dtype == torch.uint8 and dst.is_cuda and
+                dst.device == self.P.torch_device and dst.is_contiguous()):
+            raise ValueError("dst must be a contiguous uint8 CUDA tensor on the parser's device")
+        if dst.numel() < n * stride:
+            raise ValueError(f"dst holds {dst.numel()} bytes, {n} packets at stride {stride} need {n * stride}")
         vp = (ctypes.c_void_p * max(1, len(self.fields)))()
         for i, f in enumerate(self.fields):
             t = (values or {}).get(i) if f.kind == "values" else None
             if t is not None:  # (a missing array is reported by pkt_gen_run)
-                assert t.dtype == torch.uint64 and t.is_cuda and t.numel() >= n
+                if not (isinstance(t, torch.Tensor) and t.dtype == torch.uint64 and t.is_cuda and
+                        t.device == self.P.torch_device and t.is_contiguous()):
+                    raise ValueError(f"values[{i}] must be a contiguous uint64 CUDA tensor on the parser's device")
+                if t.numel() < n:
+                    raise ValueError(f"values[{i}] holds {t.numel()} values, {n} packets need {n}")
                 vp[i] = t.data_ptr()
         self.P._check(self._L.pkt_gen_run(self._h, int(first), int(n), int(stride), vp,
                                           ctypes.c_void_p(dst.data_ptr()), self.P._stream(stream)),
@@ -148,11 +159,13 @@ UDP_FIELDS = {
 def gen_udp(parser, n, fields, stride=64, template=None, stream=None):
     """n Ether/IPv4/UDP packets on the device in one pass: the template with every field in
     `fields` ({name in UDP_FIELDS: uint64 device tensor [n]}) set per packet and the IPv4
-    checksum refreshed.  Returns the flat uint8 device slab."""
-    tpl = template if template is not None else udp_template()
-    names = list(fields)
-    g = Generator(parser, tpl, [Field(*UDP_FIELDS[k]) for k in names], csum=[0])
-    try:
-        return g.run(n, stride, values={i: fields[k] for i, k in enumerate(names)}, stream=stream)
-    finally:
-        g.close()
+    checksum refreshed.  Returns the flat uint8 device slab.  The Generator of each (template,
+    field set) is created once per parser and reused: pkt_gen_create parses the template and
+    synchronises the device, which must stay off a generation loop."""
+    tpl = bytes(template if template is not None else udp_template())
+    names = tuple(fields)
+    cache = parser.__dict__.setdefault("_gen_udp_cache", {})
+    g = cache.get((tpl, names))
+    if g is None:
+        g = cache[(tpl, names)] = Generator(parser, tpl, [Field(*UDP_FIELDS[k]) for k in names], csum=[0])
+    return g.run(n, stride, values={i: fields[k] for i, k in enumerate(names)}, stream=stream)

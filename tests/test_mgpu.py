@@ -31,18 +31,52 @@ def test_packed_layout_matches_schema():
         nb = ctypes.c_uint64()
         base = 1 << 20
         assert L.pkt_out_packed(mask, n, ctypes.c_void_p(base), ctypes.byref(o), ctypes.byref(nb)) == 0
-        off = 0
-        for c in schema.COLUMN_NAMES:
+        off, at = 0, {}
+        slot = ("hdr_type", "hdr_off")  # the slot columns come last (ABI v4)
+        for c in [c for c in schema.COLUMN_NAMES if c not in slot] + list(slot):
             p = getattr(o, c)
             if c not in cols:
                 assert p is None, c
                 continue
             assert p == base + off, (c, p - base, off)
+            at[c] = off
             sz = int(np.prod(schema.column_shape(c, n))) * schema.column_dtype(c).itemsize
             off += (sz + 255) // 256 * 256
         assert nb.value == off
         assert L.pkt_out_mask(ctypes.byref(o)) == mask
+        # the pieces that hold every column with `rows` slot rows
+        rows = int(rng.integers(0, schema.MAX_HDRS + 1))
+        po, pl, npc = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_int()
+        assert L.pkt_out_packed_pieces(mask, n, rows, po, pl, ctypes.byref(npc)) == 0
+        covered = np.zeros(off, bool)
+        for k in range(npc.value):
+            covered[po[k]:po[k] + pl[k]] = True
+        need = np.zeros(off, bool)
+        for c in cols:
+            sz = int(np.prod(schema.column_shape(c, n))) * schema.column_dtype(c).itemsize
+            if c in slot:
+                sz = rows * n * schema.column_dtype(c).itemsize
+            need[at[c]:at[c] + sz] = True
+        assert not (need & ~covered).any(), (cols, n, rows)
+        moved = sum(pl[k] for k in range(npc.value))
+        slack = 255 * (len(cols) + 1)
+        assert moved <= need.sum() + slack, (moved, need.sum())
+        assert npc.value == (2 if ("hdr_type" in cols and "hdr_off" in cols and rows and n) else 1)
     assert L.pkt_out_packed(1 << 49, 10, None, None, ctypes.byref(nb)) != 0
+    po, pl, npc = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_int()
+    assert L.pkt_out_packed_pieces(1, 10, schema.MAX_HDRS + 1, po, pl, ctypes.byref(npc)) != 0
+
+
+def test_packed_pieces_c2_bytes_per_packet():
+    """a C2 shard's chain + Ether/IPv4/UDP tuples with their 3 used slot rows are
+    69 B per packet (+ 256-B column alignment), not the 108 B of all 16 rows."""
+    L = _L()
+    n = 1 << 21
+    cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+    po, pl, npc = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_int()
+    assert L.pkt_out_packed_pieces(schema.column_mask(cols), n, 3, po, pl, ctypes.byref(npc)) == 0
+    moved = sum(pl[k] for k in range(npc.value))
+    assert 69 * n <= moved <= 69 * n + 256 * len(cols), moved / n
 
 
 def test_shard_range_matches_dist():
@@ -145,3 +179,27 @@ def test_mgpu_parse_only_and_entries(MP):
         _compare(v, sub, "parse_ipv4 shard")
         lo += ni
     assert lo == n
+
+
+@pytest.mark.gpu
+def test_mgpu_orders_after_torch_stream(MP):
+    """a shard produced asynchronously on torch's stream (a Generator.run slab) goes
+    straight into parse_gather, and the gathered columns are read back through torch (.cpu() on
+    torch's current stream) with no explicit synchronisation in between."""
+    import torch
+    from pktgpu import Parser, pktgen
+    P = Parser(MP.devices[0])
+    n, stride = 1 << 16, 64
+    g = pktgen.Generator(P, pktgen.udp_template(), [pktgen.Field("IPv4", "src", kind="random", base=11),
+                                                    pktgen.Field("UDP", "dst", kind="inc", step=7)], csum=[0])
+    cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+    for rep in range(3):
+        torch.cuda.current_stream(MP.torch_devices[0]).synchronize()
+        slab = g.run(n, stride, first=rep * n)            # queued on torch's stream, not waited for
+        shards = [(slab, n, stride, None, None)]
+        views, recv, _ = MP.parse_gather(shards, columns=cols, merge=True)
+        got = {k: v.cpu().numpy() for k, v in views.items()}  # torch's stream waits for the gather
+        ref = oracle.parse_batch(slab.cpu().numpy(), n, stride=stride, columns=cols, nthreads=8)
+        _compare(got, ref, f"generator -> parse_gather rep {rep}")
+    g.close()
+    P.close()
