@@ -4,20 +4,24 @@
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2|c3|c4]
   python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
-A step = one pkt_parse_batch launch over one batch of 2^20 packets (config C2 by default:
-64-byte Ether/IPv4/UDP, fixed stride) producing the chain + Ether/IPv4/UDP field tuple +
-recomputed IPv4 checksum.  Each step reads a different slab of a >= 1 GiB ring (and writes a
-different output set), so the 256 MiB Infinity Cache cannot serve the working set.  Inputs are
-resident in HBM before the timed region starts.
+A step = one parse of one batch of 2^20 packets per GPU (config C2 by default: 64-byte
+Ether/IPv4/UDP, fixed stride) producing the chain + Ether/IPv4/UDP field tuple + recomputed IPv4
+checksum.  Each step reads a different slab of a >= 1 GiB ring per GPU (and writes a different
+output set), so the 256 MiB Infinity Cache cannot serve the working set.  Inputs are resident in
+HBM before the timed region starts.
 
-Multi-GPU, one process per GPU: under torch.distributed.run the ranks come from the environment;
-`python bench.py --gpus N` (N > 1) starts the N ranks itself (one child per device, spawned before
-anything touches the GPU) and fails if fewer than N devices are visible.  Every rank parses its
-own 2^20-packet batch per step (weak scaling, no collective in the step).  A second record ("c5")
-times the C5 config: 2^24 packets in total, split in contiguous shards over the ranks (strong
-scaling), and the RCCL gather of the shards' packed tuple buffers to rank 0 — timed separately.
+Multi-GPU = the library's own multi-device entry (include/pktgpu.h pkt_mgpu_*): ONE process drives
+the N devices, the K steps go out through pkt_mgpu_parse_steps (one issuing host thread per device,
+2 streams per device), weak scaling: every device parses its own 2^20-packet batch per step with no
+exchange (fast::parse is a pure function of one packet, reference src/parser/fast.rs:5-12).  Under
+torch.distributed.run rank 0 is that process and the other ranks wait at a CPU (gloo) barrier
+without touching a GPU.  The "c5" record times the C5 config through pkt_mgpu_parse_gather: 2^24
+packets in contiguous shards, parse and RCCL gather of the used tuple bytes to device 0 timed
+separately.  --per-rank keeps the one-process-per-GPU torch.distributed form.
+At N = 1 the line also carries the host-memory rate ("host": pinned zero-copy pkt_parse_host) and
+the capture path ("pcap": capture in HBM -> pkt_pcap_index_device -> parse, one step).
 
-Prints ONE JSON line on rank 0 (see DESIGN.md "Measurement" for every field).
+Prints ONE JSON line (see DESIGN.md "Measurement" for every field).
 """
 import argparse
 import json
@@ -60,7 +64,10 @@ def parse_args():
     ap.add_argument("--window", type=int, default=int(os.environ.get("PKTGPU_WINDOW", "0")),
                     help="pkt_ctx_set_window bytes (0 = auto)")
     ap.add_argument("--streams", type=int, default=2,
-                    help="consecutive steps are issued round-robin on this many HIP streams")
+                    help="consecutive steps are issued round-robin on this many HIP streams per device")
+    ap.add_argument("--per-rank", action="store_true",
+                    help="one process per GPU with torch.distributed (the round-2 form) instead of pkt_mgpu")
+    ap.add_argument("--no-extra", action="store_true", help="skip the host and pcap records (N = 1)")
     return ap.parse_args()
 
 
@@ -289,35 +296,438 @@ def run_c5(args, torch, dist, P, world, rank, dev, cols, d_first, entry):
            "scaling": "strong", "packets_per_gpu": n5, "steps": K,
            "ms_per_step": round(el / K * 1e3, 5), "Gpkt/s": round(args.total_packets * K / el / 1e9, 4)}
     if world > 1:
-        buf = outs[0][0] if args.backend == "nccl" else outs[0][0].cpu()
-        nmax = pdist.shard_range(args.total_packets, world, 0)[1]  # shard 0 is the largest
+        # the used tuple bytes only: the packed buffer's pieces with the batch's used slot rows
+        # (pkt_out_packed_pieces), each padded to the largest shard's for dist.gather
         from pktgpu import mgpu
-        cap = mgpu.packed_bytes(cols, nmax)
-        if buf.numel() < cap:  # equal-size messages for dist.gather
-            pad = torch.zeros(cap, dtype=torch.uint8, device=buf.device)
-            pad[:buf.numel()] = buf
-            buf = pad
-        glist = [torch.empty_like(buf) for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, glist, dst=0)  # warm (communicator + channels)
+        rows = int(outs[0][1]["n_hdrs"].max().item()) if "n_hdrs" in outs[0][1] else 16
+        rows = int(max_over_ranks(torch, dist, world, rows, dev, args.backend))
+        nmax = pdist.shard_range(args.total_packets, world, 0)[1]  # shard 0 is the largest
+        po, pl = mgpu.packed_pieces(cols, n5, rows)
+        _, plmax = mgpu.packed_pieces(cols, nmax, rows)
+        src = outs[0][0] if args.backend == "nccl" else outs[0][0].cpu()
+        bufs = []
+        for k in range(len(po)):
+            b = torch.zeros(plmax[k], dtype=torch.uint8, device=src.device)
+            b[:pl[k]] = src[po[k]:po[k] + pl[k]]
+            bufs.append(b)
+        glists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in bufs]
+
+        def gather():
+            for b, gl in zip(bufs, glists):
+                dist.gather(b, gl, dst=0)
+
+        gather()  # warm (communicator + channels)
         sync_barrier(torch, dist, world)
         G = 5
         tg = time.perf_counter()
         for _ in range(G):
-            dist.gather(buf, glist, dst=0)
+            gather()
         sync_barrier(torch, dist, world)
         gs = max_over_ranks(torch, dist, world, (time.perf_counter() - tg) / G, dev, args.backend)
-        into_root = buf.numel() * (world - 1)
+        into_root = sum(b.numel() for b in bufs) * (world - 1)
         rec["gather"] = {"ms": round(gs * 1e3, 4), "bytes_into_root": into_root,
                          "GB/s_into_root": round(into_root / gs / 1e9, 2),
-                         "message": "one packed tuple buffer per rank (pkt_out_packed layout)",
+                         "message": f"the packed tuple buffer's {len(bufs)} used piece(s) per rank "
+                                    f"({rows} slot rows, pkt_out_packed_pieces)",
                          "backend": "nccl (RCCL over xGMI)" if args.backend == "nccl" else args.backend,
                          "parse_plus_gather_ms": round(el / K * 1e3 + gs * 1e3, 4)}
     return rec
 
 
-# ------------------------------------------------------------------------------ one rank
+# ------------------------------------------------------------------------------ shared pieces
+DEFAULT_COLS = {"c2": "chain,ether,ipv4,udp", "c3": "chain,ether,vlan,ipv4,tcp,udp", "c4": "all",
+                "c5": "chain,ether,ipv4,udp"}
+WORKLOAD = {"c2": "C2: 2^20 x 64 B Ether/IPv4/UDP fixed-stride slab per GPU",
+            "c3": "C3: 2^20 x 128 B Ether/{0-2}xVlan/IPv4/TCP|UDP per GPU",
+            "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}
+
+
+def roofline_phase(args, torch, P, batches, ostructs, raw_slabs, ring, n, stride, entry, default_cols, dev):
+    """The parse kernel in isolation on device 0 — R back-to-back launches on ONE stream between one
+    event pair on that stream — alternated with the ceiling probe (same launch shape, same bytes, no
+    parsing; C2-shaped configs only) and a device copy of the slab.  Median of 5 rounds each."""
+    import ctypes
+    R = min(max(args.steps, 20), 50)
+    rs = torch.cuda.Stream(dev)
+    probe = load_probe() if (args.config in ("c2", "c5") and args.columns == default_cols) else None
+
+    def parse_launch(k, s):
+        P.launch(batches[k % ring], entry, ostructs[k % ring], s)
+
+    def probe_launch(k, s):
+        rc = probe.pkt_probe_ceiling(ctypes.c_void_p(raw_slabs[k % ring].data_ptr()), n, stride,
+                                     ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
+        if rc != 0:
+            raise RuntimeError(f"pkt_probe_ceiling failed ({rc})")
+
+    copy_dst = torch.empty_like(raw_slabs[0])
+
+    def copy_launch(k, s):
+        with torch.cuda.stream(s):
+            copy_dst.copy_(raw_slabs[k % ring])
+
+    kern, ceil_, copy_ = [], [], []
+    for _ in range(5):
+        kern.append(event_avg_ms(torch, rs, parse_launch, R))
+        if probe is not None:
+            ceil_.append(event_avg_ms(torch, rs, probe_launch, R))
+        copy_.append(event_avg_ms(torch, rs, copy_launch, R))
+    del copy_dst
+    # the probe overwrote output sets: re-parse them so the outputs are real
+    for r in range(ring):
+        parse_launch(r, rs)
+    torch.cuda.synchronize(dev)
+    return R, kern, ceil_, copy_
+
+
+def assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, slab_bytes, stride, offs_np, span,
+             pipe_s):
+    """The roofline / line-floor / traffic objects of the JSON line."""
+    algo = read_b + write_b
+    avg_kern_s = float(np.median(kern)) * 1e-3
+    achieved = algo / avg_kern_s / 1e9
+    res["roofline"] = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
+                       "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                       "frac_kind": "kernel: algorithmic bytes / isolated launch duration (HIP events, "
+                                    "one stream) / 8 TB/s spec",
+                       "kernel": "parse_kernel", "avg_kernel_us": round(avg_kern_s * 1e6, 3),
+                       "read_only_frac": round(read_b / avg_kern_s / 1e9 / HBM_PEAK_GBS, 4),
+                       "measured": f"device 0: median of 5 rounds of {R} back-to-back launches on one "
+                                   f"stream, one HIP event pair per round",
+                       "algorithmic_bytes_per_launch": algo,
+                       "pipelined": {"streams": args.streams,
+                                     "device_ms_per_step": round(pipe_s * 1e3, 5),
+                                     "achieved": round(algo / pipe_s / 1e9, 2),
+                                     "frac": round(algo / pipe_s / 1e9 / HBM_PEAK_GBS, 4),
+                                     "frac_kind": "throughput: algorithmic bytes per step / device-0 time "
+                                                  "per step of the timed region (HIP events) / 8 TB/s"}}
+    if ceil_:
+        cs = float(np.median(ceil_)) * 1e-3
+        res["roofline"]["ceiling"] = {
+            "kernel": "pkt_probe_ceiling (libpktprobe.so): same launch shape and bytes, no parsing",
+            "avg_kernel_us": round(cs * 1e6, 3), "achieved": round(algo / cs / 1e9, 2),
+            "frac_of_peak": round(algo / cs / 1e9 / HBM_PEAK_GBS, 4),
+            "parse_frac_of_ceiling": round(cs / avg_kern_s, 4)}
+    # the line-granular floor: distinct 128-B lines holding header bytes + the batch index read
+    # + the columns written, priced at this box's measured copy rate (DESIGN.md §5)
+    idx_b = 12 * n if offs_np is not None else 0
+    floor_b = line_bytes(n, stride, offs_np, span) + idx_b + write_b
+    copy_gbs = 2 * slab_bytes / (float(np.median(copy_)) * 1e-3) / 1e9
+    floor_s = floor_b / (copy_gbs * 1e9)
+    res["roofline"]["line_floor"] = {
+        "bytes_per_launch": floor_b, "read_lines": floor_b - idx_b - write_b, "index_read": idx_b,
+        "written": write_b, "copy_rate_GBps": round(copy_gbs, 2),
+        "copy": "torch copy_ of the slab over the same ring (read + write), HIP events, one stream",
+        "floor_us_at_copy_rate": round(floor_s * 1e6, 3),
+        "kernel_frac_of_floor": round(floor_s / avg_kern_s, 4),
+        "pipelined_frac_of_floor": round(floor_s / pipe_s, 4)}
+    # HBM traffic per launch from the committed rocprofv3 PMC passes of this config, if any
+    tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
+    if os.path.exists(tpath) and args.columns == DEFAULT_COLS[args.config] and n == 1 << 20:
+        t = json.load(open(tpath))
+        res["roofline"]["traffic"] = t["traffic_bytes_per_launch"]
+        res["roofline"]["traffic_source"] = {
+            "measured_in_this_run": False,
+            "file": f"profiles/traffic_{args.config}.json",
+            "how": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes of "
+                   "this bench command (scripts/gpu_round.sh)",
+            "x2_check": "every memory-side read request of these launches is a 128-B line "
+                        "(TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; FETCH_SIZE counts 64 B per request): "
+                        "profiles/ab/r02calib_fetch_requests.txt",
+            "run": t.get("label", "")}
+
+
+def host_record(P, torch, cols, n=1 << 20, reps=5):
+    """The host-memory path (north_star: the path starts and ends in host memory): a pinned C2
+    batch and pinned columns through pkt_parse_host, which reads the slab and writes the columns
+    over PCIe directly (zero copy, one launch); blocking per batch."""
+    from pktgpu import gen
+    slab = P.host_empty((n * 64,), np.uint8)
+    slab[:] = gen.gen_c2(n, seed=0x5EED0004).reshape(-1)
+    from pktgpu import schema
+    out = {c: P.host_empty(schema.column_shape(c, n), schema.column_dtype(c)) for c in cols}
+    P.parse_host(slab, stride=64, columns=cols, out=out)  # warm (code object, mapping)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        P.parse_host(slab, stride=64, columns=cols, out=out)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    used = int(out["n_hdrs"].max()) if "n_hdrs" in out else schema.MAX_HDRS
+    written = schema.bytes_per_packet(cols, n_slots=used) * n
+    return {"workload": "C2 2^20 x 64 B in pinned host memory -> pinned host columns (chain+ether+ipv4+udp)",
+            "entry": "pkt_parse_host (zero copy: every buffer from pkt_host_alloc)",
+            "ms_per_batch": round(t * 1e3, 4), "Gpkt/s": round(n / t / 1e9, 4),
+            "link_GB/s": {"host_to_device": round(64 * n / t / 1e9, 2),
+                          "device_to_host": round(written / t / 1e9, 2)},
+            "reps": reps, "timing": "wall clock per blocking call, median"}
+
+
+def pcap_record(P, torch, dev, n=1 << 20, reps=10):
+    """The capture path of tests/pcap.rs:7-37 on the device as one step: a pcap file already in HBM
+    -> pkt_pcap_index_device (record boundaries) -> pkt_parse_batch of every record (all columns)."""
+    import ctypes
+    from pktgpu import gen, schema
+    buf, offs, lens = gen.gen_c4(n, seed=0x5EED0005)
+    d_buf = torch.from_numpy(buf).to(dev)
+    d_offs = torch.empty(n, dtype=torch.uint64, device=dev)
+    d_lens = torch.empty(n, dtype=torch.uint32, device=dev)
+    cols = schema.COLUMN_NAMES
+    out = P.alloc(n, cols)
+    ostr = P.out_struct(out)
+    s = torch.cuda.current_stream(dev)
+    cnt = ctypes.c_uint64()
+
+    def step():
+        P._check(P._L.pkt_pcap_index_device(P._ctx, d_buf.data_ptr(), d_buf.numel(), d_offs.data_ptr(),
+                                             d_lens.data_ptr(), n, ctypes.byref(cnt), P._stream(s)),
+                 "pkt_pcap_index_device")
+        P.launch(P._batch(d_buf, int(cnt.value), None, d_offs, d_lens), 0, ostr, s)
+        s.synchronize()
+
+    step()
+    ok = int(cnt.value) == n and np.array_equal(d_offs.cpu().numpy(), offs)
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        step()
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"workload": f"C4 capture: {n} records of the 22 reference templates, {buf.size} B pcap file in HBM",
+            "step": "pkt_pcap_index_device (blocking: its record count comes back to the host) + "
+                    "pkt_parse_batch (all columns) + stream sync",
+            "ms_per_step": round(t * 1e3, 4), "Grecords/s": round(n / t / 1e9, 4),
+            "file_GB/s": round(buf.size / t / 1e9, 2), "index_matches_host_indexer": bool(ok),
+            "reps": reps, "timing": "wall clock per step, median"}
+
+
+# ------------------------------------------------------------------------------ the library's multi-GPU entry
+def run_mgpu(args, ndev):
+    """One process, ndev devices through pkt_mgpu (the measured form for every N)."""
+    import torch
+    visible = torch.cuda.device_count()
+    if visible < ndev:
+        print(f"bench.py: --gpus {ndev} but only {visible} device(s) visible", file=sys.stderr)
+        sys.exit(2)
+    import pktgpu
+    from pktgpu import mgpu, schema
+    torch.cuda.set_device(0)
+    devices = list(range(ndev))
+    MP = mgpu.MultiParser(devices)
+    MP.set_knobs(fastpath=args.fastpath, staging=args.staging, window=args.window)
+    default_cols = DEFAULT_COLS[args.config]
+    if args.columns is None:
+        args.columns = default_cols
+    cols = pktgpu.resolve_columns("all" if args.columns == "all" else args.columns.split(","))
+    entry = schema.ENTRY_ID["parse"]
+    n = args.packets
+
+    # ---------------- inputs: one seeded batch per device, replicated over a >= ring_gib ring
+    per = []
+    for i, d in enumerate(MP.torch_devices):
+        slab_np, stride, offs_np, lens_np = make_input(args.config, n, seed=0x5EED0000 + 2 + i)
+        ring = max(2, int(np.ceil(args.ring_gib * (1 << 30) / slab_np.size)))
+        first = torch.from_numpy(slab_np).to(d)
+        slabs = [first] + [first.clone() for _ in range(ring - 1)]
+        offs = torch.from_numpy(offs_np).to(d) if offs_np is not None else None
+        lens = torch.from_numpy(lens_np).to(d) if lens_np is not None else None
+        outs = packed_outputs(torch, d, cols, n, ring)
+        per.append(dict(slab_np=slab_np, stride=stride, offs_np=offs_np, lens_np=lens_np, ring=ring,
+                        slabs=slabs, offs=offs, lens=lens, outs=outs))
+    ring = per[0]["ring"]
+    total_steps = args.warmup + args.steps
+    plan = MP.steps_plan([[((pd["slabs"][k % ring], n, pd["stride"], pd["offs"], pd["lens"]), pd["outs"][k % ring][0])
+                           for pd in per] for k in range(total_steps)])
+    if args.warmup:
+        MP.parse_steps(plan, entry, cols, first=0, count=args.warmup, streams=args.streams)
+    MP.synchronize()
+
+    # ---------------- timed region: K steps on every device (pkt_mgpu_parse_steps), all devices
+    # idle on both sides; one event pair on device 0's work stream (the extra streams start after
+    # and are joined back into it) gives device 0's time per step
+    ext0 = MP.streams()[0]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record(ext0)
+    MP.parse_steps(plan, entry, cols, first=args.warmup, count=args.steps, streams=args.streams)
+    e1.record(ext0)
+    MP.synchronize()
+    elapsed = time.perf_counter() - t0
+    region_ms = e0.elapsed_time(e1)
+
+    # ---------------- roofline sub-phase on device 0 (its own ctx, same buffers)
+    P = pktgpu.Parser(0)
+    P.set_fastpath(args.fastpath)
+    P.set_staging(args.staging)
+    P.set_window(args.window)
+    p0 = per[0]
+    batches0 = [P._batch(p0["slabs"][r], n, p0["stride"], p0["offs"], p0["lens"]) for r in range(ring)]
+    ostructs0 = [P.out_struct(p0["outs"][r][1]) for r in range(ring)]
+    R, kern, ceil_, copy_ = roofline_phase(args, torch, P, batches0, ostructs0, p0["slabs"], ring, n, p0["stride"],
+                                           entry, default_cols, MP.torch_devices[0])
+
+    c5 = None
+    if args.config == "c2" and not args.no_c5:
+        c5 = run_c5_mgpu(args, torch, MP, per, cols, entry)
+
+    o0 = p0["outs"][0][1]
+    used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
+    span = o0["payload_off"].cpu().numpy() if "payload_off" in o0 else np.full(n, 64, np.int64)
+    read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
+    algo = read_b + write_b
+    slab_bytes = p0["slab_np"].size
+    value = ndev * n * args.steps / elapsed / 1e9
+    pipe_s = region_ms * 1e-3 / args.steps
+    agg_gbs = algo * ndev * args.steps / elapsed / 1e9
+    res = {
+        "metric": METRIC,
+        "value": round(value, 4),
+        "unit": "Gpkt/s",
+        "n_gpus": ndev,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded generator, pktgpu/gen.py)",
+        "config": {
+            "workload": WORKLOAD[args.config],
+            "packets_per_gpu": n, "entry": "fast::parse", "columns": args.columns,
+            "ring_slabs": ring, "ring_bytes": ring * slab_bytes, "parallelism": f"dp{ndev}",
+            "launch": f"pkt_mgpu_parse_steps: one process, {ndev} device(s), one issuing host thread per "
+                      f"device, {args.streams} streams per device",
+            "staging": args.staging, "window": args.window,
+        },
+        "GB/s": {"algorithmic": round(agg_gbs, 2),
+                 "slab": round(slab_bytes * ndev * args.steps / elapsed / 1e9, 2),
+                 "algorithmic_bytes_per_pkt": {"read": read_b / n, "written": write_b / n},
+                 "aggregate_frac_of_n_x_peak": round(agg_gbs / (ndev * HBM_PEAK_GBS), 4)},
+    }
+    assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, slab_bytes, p0["stride"],
+             p0["offs_np"], span, pipe_s)
+    res["timing"] = {"wall_ms": round(elapsed * 1e3, 4), "device0_region_ms": round(region_ms, 4),
+                     "outside_device_region_ms": round(elapsed * 1e3 - region_ms, 4)}
+    if c5 is not None:
+        res["c5"] = c5
+    if ndev == 1 and not args.no_extra:
+        res["host"] = host_record(P, torch, cols)
+        res["pcap"] = pcap_record(P, torch, MP.torch_devices[0])
+    if ndev == 1 and not args.no_cpu_baseline:
+        cores, aff, quota = host_cores()
+        threads = args.cpu_threads or cores
+        res["cpu_baseline"] = cpu_baseline(p0["slab_np"], p0["stride"], p0["offs_np"], p0["lens_np"], n, cols, threads)
+        res["cpu_baseline"]["host"] = {"affinity_cpus": aff, "cgroup_cpu_quota": quota,
+                                       "os_cpu_count": os.cpu_count()}
+    P.close()
+    MP.close()
+    return res
+
+
+def run_c5_mgpu(args, torch, MP, per, cols, entry):
+    """C5: args.total_packets 64-B packets in contiguous shards over the devices (strong scaling):
+    K parse steps through pkt_mgpu_parse_steps, then pkt_mgpu_parse_gather (merge = 0) to device 0,
+    which moves each shard's packed tuples with only its used slot rows; parse and parse + gather
+    timed separately (wall clock around each, devices idle on both sides)."""
+    from pktgpu import dist as pdist, mgpu, schema
+    nd = MP.ndev
+    shards, outs = [], []
+    ring = 2
+    for i, pd in enumerate(per):
+        lo, hi = pdist.shard_range(args.total_packets, nd, i)
+        ni = hi - lo
+        first = pd["slabs"][0]
+        reps = -(-ni // (first.numel() // 64))
+        base = first.repeat(reps)[:ni * 64].contiguous()
+        slabs = [base] + [base.clone() for _ in range(ring - 1)]
+        shards.append([(s, ni, 64, None, None) for s in slabs])
+        outs.append([torch.empty(max(1, mgpu.packed_bytes(cols, ni)), dtype=torch.uint8, device=base.device)
+                     for _ in range(ring)])
+    K = max(4, min(args.steps, 20))
+    plan = MP.steps_plan([[(shards[i][k % ring], outs[i][k % ring]) for i in range(nd)] for k in range(K + 2)])
+    MP.parse_steps(plan, entry, cols, first=0, count=2, streams=args.streams)
+    MP.synchronize()
+    t0 = time.perf_counter()
+    MP.parse_steps(plan, entry, cols, first=2, count=K, streams=args.streams)
+    MP.synchronize()
+    el = time.perf_counter() - t0
+    rec = {"workload": f"C5: {args.total_packets} x 64 B Ether/IPv4/UDP, contiguous shards over {nd} GPU(s)",
+           "scaling": "strong", "packets_per_gpu": [s[0][1] for s in shards], "steps": K,
+           "ms_per_step": round(el / K * 1e3, 5), "Gpkt/s": round(args.total_packets * K / el / 1e9, 4)}
+    # parse + gather (one step, blocking), and the parse alone the same way
+    one = [shards[i][0] for i in range(nd)]
+    recv = torch.empty(MP.recv_bytes(one, cols, False), dtype=torch.uint8, device=MP.torch_devices[0])
+    sh_out = [outs[i][0] for i in range(nd)]
+    MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)  # warm (RCCL channels)
+    MP.synchronize()
+    tp, tg = [], []
+    for _ in range(5):
+        t0 = time.perf_counter()
+        MP.parse(one, columns=cols, shard_out=sh_out)
+        MP.synchronize()
+        tp.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)
+        MP.synchronize()
+        tg.append(time.perf_counter() - t0)
+    parse_s, pg_s = float(np.median(tp)), float(np.median(tg))
+    rows = int(max(int(o["n_hdrs"].max().item()) for o in
+                   [mgpu.packed_views(sh_out[i], cols, one[i][1]) for i in range(nd)]))
+    moved = []
+    for i in range(nd):
+        po, pl = mgpu.packed_pieces(cols, one[i][1], rows)
+        moved.append(sum(pl))
+    into_root = sum(moved[1:])
+    gather_s = max(pg_s - parse_s, 1e-9)
+    rec["gather"] = {"entry": "pkt_mgpu_parse_gather (merge = 0, root = device 0)",
+                     "parse_ms": round(parse_s * 1e3, 4), "parse_plus_gather_ms": round(pg_s * 1e3, 4),
+                     "gather_ms": round(gather_s * 1e3, 4),
+                     "bytes_per_pkt_moved": round(sum(moved) / args.total_packets, 2),
+                     "slot_rows_moved": rows,
+                     "bytes_into_root": into_root,
+                     "GB/s_into_root": round(into_root / gather_s / 1e9, 2) if into_root else None,
+                     "bytes_root_local": moved[0],
+                     "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI)",
+                     "timing": "wall clock around each blocking call (+ synchronize), median of 5; "
+                               "gather = (parse + gather) - parse"}
+    return rec
+
+
+# ------------------------------------------------------------------------------ entry
 def main():
     args = parse_args()
+    if args.per_rank:
+        return main_per_rank(args)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    ndev = world if world > 1 else args.gpus
+    if world > 1 and world != args.gpus and rank == 0:
+        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
+    dist = None
+    if world > 1:
+        # launched as one process per GPU: rank 0 drives all `world` devices through pkt_mgpu, the
+        # other ranks wait here without touching a GPU (CPU barrier)
+        import datetime
+        import torch.distributed as dist
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=30))
+        if rank != 0:
+            dist.barrier()
+            dist.destroy_process_group()
+            return
+    try:
+        res = run_mgpu(args, ndev)
+    finally:
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+    print(json.dumps(res), flush=True)
+
+
+# ------------------------------------------------------------------------------ one process per GPU (--per-rank)
+def main_per_rank(args):
+    """The round-2 form: one process per GPU (bench.py spawns them, or torch.distributed.run), every
+    rank parses its own batch per step through the single-device entry, max over ranks."""
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -480,6 +480,13 @@ void       *pkt_mgpu_stream(pkt_mgpu_t *mg, int shard);
  * (device memory of devices[i], pkt_out_packed(col_mask, batches[i].n) bytes). */
 int pkt_mgpu_parse(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
                    void *const *shard_out);
+/* `steps` consecutive pkt_mgpu_parse calls in one: step k parses batches[k*ndev + i] into the packed
+ * buffer shard_out[k*ndev + i] on device i.  One host thread per device issues its device's launches,
+ * round-robin over `streams` (1..4) streams of that device which start after, and are joined back
+ * into, its work stream (steps are independent: different inputs, different outputs), so the launch
+ * rate scales with the device count.  Asynchronous: returns after the launches. */
+int pkt_mgpu_parse_steps(pkt_mgpu_t *mg, const pkt_batch_t *batches, int steps, int entry, uint64_t col_mask,
+                         void *const *shard_out, int streams);
 /* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
  * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.
  * Grouped ncclSend/ncclRecv (the root's own block is a send to itself). */

@@ -180,8 +180,6 @@ __host__ __device__ constexpr uint32_t lane_stride(int nch) { return (uint32_t)(
 __host__ __device__ constexpr size_t window_lds(int nch) {
     return ((size_t)kBlock * lane_stride(nch) + 16 + 15) & ~(size_t)15;
 }
-// the lockstep walk's first-offset slots: u16 [type 0..7][lane], after the windows / the span region
-constexpr size_t first_lds(uint32_t lanes) { return 8u * lanes * sizeof(uint16_t); }
 
 __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
                                                 uint32_t len, int nch) {
@@ -225,11 +223,7 @@ __device__ __forceinline__ void load_packet(const KParams& p, uint32_t i, bool a
     for (int c = 0; c < NCH; c++) {
         uint64_t o = a0 + 16u * (uint32_t)c;
         o = o > last16 ? last16 : o;
-#if PKTGPU_NT_LOAD
-        chunk[c] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p.slab + o));
-#else
         chunk[c] = *reinterpret_cast<const u32x4*>(p.slab + o);
-#endif
     }
 }
 
@@ -254,17 +248,12 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
 // One block = 256 packets, one lane per packet.  (A persistent grid of k blocks per CU striding
 // over the tiles, each lane's loads of its next packet in flight while it parsed the current one,
 // was measured no faster at k = 4 and slower at k = 1, 2: DESIGN.md §5.)
-#ifndef PKTGPU_WAVES_PER_EU
-#define PKTGPU_WAVES_PER_EU 8  // 8 resident waves per SIMD (<= 64 VGPRs); wide windows (NCH > 9) unconstrained
-#endif
-#ifndef PKTGPU_COOP_ALL
-#define PKTGPU_COOP_ALL 1  // every window chunk cooperative (0: chunks 0-3 cooperative, 4.. per lane)
-#endif
-#ifndef PKTGPU_COOP_FIXED
-#define PKTGPU_COOP_FIXED 1  // fixed-stride batches load their windows cooperatively too
-#endif
+// Resident waves per SIMD the compiler may assume (VGPR budget 512 / waves): 8 for fixed-stride
+// windows (<= 64 VGPRs); 4 for the 144-byte indexed windows, whose 37.9 KB of LDS per block allows 4
+// blocks per CU anyway; wider windows unconstrained.
+__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch == 9 ? 4 : 8); }
 template <int NCH, uint32_t GM, int WK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(NCH <= 9 ? PKTGPU_WAVES_PER_EU : 1)))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
 void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
@@ -272,32 +261,32 @@ void parse_kernel(KParams p) {
     u32x4 chunk[NCH];
     uint64_t off;
     uint32_t len;
-    if constexpr (NCH >= 4 && (WK == 1 || PKTGPU_COOP_FIXED)) {
-        // The wave loads its 64 windows cooperatively — in load k, lanes 4j..4j+3
-        // fetch chunks 0-3 of packet 16k + j, i.e. 64 contiguous bytes per 4 lanes instead of one
-        // scattered 16-byte piece per lane (the per-lane shape is request-bound: 42 us for the
-        // 2^20 C4 windows alone, scripts/probe_c4.py) — and writes them straight into the owning
-        // lane's LDS window; chunks 4.. are loaded per lane.  C4, 2^20 records, same box: pipelined
-        // 78 vs 82 us/step (all columns), 52 vs 55 (chain); isolated status-only 64 vs 70 us
-        // (profiles/ab/r02p_c4_coop_windows.txt).  Fixed-stride batches the same way (the fast
-        // path then classifies from the lane's LDS window): C2 pipelined 23.9 vs 25.2 us/step, C3
-        // 43.3 vs 46.1 (profiles/ab/r02x_coop_fixed_stride.txt).
+    if constexpr (NCH >= 4) {
+        // The wave loads its 64 windows cooperatively: the 64*NCH (packet, chunk) pairs, pair
+        // 64k + lane in load k, so consecutive lanes fetch consecutive 16-byte chunks of one packet
+        // and each window comes from one or two wave instructions — the per-lane shape (each lane
+        // fetching its own chunks) is request-bound, 42 us for the 2^20 C4 windows alone
+        // (scripts/probe_c4.py), and separate instructions to the same 128-B line re-request it from
+        // memory (scripts/fetch_calib.py).  Each chunk goes straight into the owning lane's LDS
+        // window.  C4 pipelined 78 vs 82 us/step, C2 23.9 vs 25.2, C3 43.3 vs 46.1 against per-lane
+        // loads (profiles/ab/r02p_c4_coop_windows.txt, r02x_coop_fixed_stride.txt).
+        // Lockstep (indexed) launches skip the chunks that start past their packet's end: their
+        // 144-byte windows hold every header of the 22 templates, and a short record (Dot3, ARP)
+        // then fetches only its own lines.
         off = 0;
         len = 0;
         if (act) packet_range(p, base + threadIdx.x, off, len);
         const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
         const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
-#if PKTGPU_COOP_ALL
-        // All NCH chunks of the wave's 64 windows as 64*NCH (record, chunk) pairs, pair 64k + lane
-        // in load k: consecutive lanes fetch consecutive chunks of one record, so each window's
-        // bytes come from one or two wave instructions instead of a cooperative 64-byte piece plus
-        // per-lane chunks (separate instructions to the same 128-B line re-request it from memory:
-        // scripts/fetch_calib.py).
 #pragma unroll
         for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
             const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
             const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
                                   (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+            if constexpr (WK == 1) {
+                const uint32_t lenr = (uint32_t)__shfl((int)len, (int)r, 64);
+                if (16u * c >= (uint32_t)(offr & 15) + lenr) continue;  // chunk past the packet
+            }
             uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
             a = a > last16 ? last16 : a;
             const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
@@ -307,33 +296,6 @@ void parse_kernel(KParams p) {
             w[2] = v.z;
             w[3] = v.w;
         }
-#else
-#pragma unroll
-        for (uint32_t k = 0; k < 4; k++) {
-            const uint32_t r = 16u * k + (wl >> 2), c = wl & 3u;
-            const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
-                                  (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
-            uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
-            a = a > last16 ? last16 : a;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
-            uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
-            w[0] = v.x;
-            w[1] = v.y;
-            w[2] = v.z;
-            w[3] = v.w;
-        }
-#pragma unroll
-        for (int c = 4; c < NCH; c++) {
-            uint64_t a = (off & ~(uint64_t)15) + 16u * (uint32_t)c;
-            a = a > last16 ? last16 : a;
-            const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
-            uint32_t* w = reinterpret_cast<uint32_t*>(lds + threadIdx.x * lane_stride(NCH)) + 4 * c;
-            w[0] = v.x;
-            w[1] = v.y;
-            w[2] = v.z;
-            w[3] = v.w;
-        }
-#endif
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -345,12 +307,6 @@ void parse_kernel(KParams p) {
 }
 
 template <int NCH, uint32_t GM, int WK, bool STAGED>
-#ifndef PKTGPU_FAST_REG
-// 1: waves whose packets all take the fast path decode from registers, no LDS.  0 (default):
-// they stage and emit through LDS like mixed waves.  C2, same box: registers 28.7 us isolated /
-// 24.0 us pipelined per step, LDS 29.8 / 23.4 — the pipelined rate is the bench's value.
-#define PKTGPU_FAST_REG 0
-#endif
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own) {
@@ -390,8 +346,8 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         }
     }
     // Fast lanes skip the walk; all lanes stage their window and emit from LDS together (one
-    // store per column per wave).  With PKTGPU_FAST_REG a wave whose every packet is fast and
-    // untagged decodes from registers instead (wave-uniform branch).
+    // store per column per wave).  (Decoding all-fast waves from registers instead: shorter
+    // isolated launches, slower pipelined steps)
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
     auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
@@ -420,32 +376,13 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         push(1 + v, PKT_HDR_IPV4, 14u + 4u * v);
         push(2 + v, fudp ? PKT_HDR_UDP : PKT_HDR_TCP, l4);
     };
-    if constexpr (NCH >= 4 && !STAGED) {
-        if (PKTGPU_FAST_REG && __ballot(fast && fv == 0) == __ballot(active_own)) {
-            if (!active_own) return;
-            RegView<NCH> rv;
-#pragma unroll
-            for (int c = 0; c < NCH; c++) {
-                rv.w[4 * c] = chunk[c].x;
-                rv.w[4 * c + 1] = chunk[c].y;
-                rv.w[4 * c + 2] = chunk[c].z;
-                rv.w[4 * c + 3] = chunk[c].w;
-            }
-            WalkResult r;
-            fast_result(r, 0u);
-            emit_chain<GM>(out, i_own, len_own, r);
-            emit_fields<GM>(out, i_own, rv, r, true);
-            return;
-        }
-    }
     if constexpr (!STAGED) stage_window<NCH>(lds, t, chunk);
     PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
 
     // each lane walks and emits its own packet (no barrier: own LDS only)
     __builtin_amdgcn_wave_barrier();
     WalkResult r;
-    walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r,
-             reinterpret_cast<uint16_t*>(lds + window_lds(NCH)) + t, (uint32_t)kBlock);
+    walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r);
     if constexpr (NCH >= 4) {
         if (fast) fast_result(r, fv);
     }
@@ -537,8 +474,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
         if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
     };
     WalkResult r;
-    walk<WK>(pv, entry_state(p.entry), active, push, r, reinterpret_cast<uint16_t*>(lds + span_region(NCH)) + lane,
-             kSpanBlock);
+    walk<WK>(pv, entry_state(p.entry), active, push, r);
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
@@ -552,9 +488,9 @@ template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
-                           dim3(kSpanBlock), span_region(NCH) + (WK ? first_lds(kSpanBlock) : 0), s, kp);
+                           dim3(kSpanBlock), span_region(NCH), s, kp);
     } else {
-        const size_t lds = window_lds(NCH) + (WK ? first_lds(kBlock) : 0);
+        const size_t lds = window_lds(NCH);
         hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }
@@ -806,9 +742,12 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Window: bytes of each packet staged in LDS.  Fixed stride: the slot (up to 128 B);
     // indexed: 128 B.  Unaligned packet starts need one more chunk.
     uint32_t w = ctx->window;
-    // Auto window: 64 bytes hold every header of the common chains (Ether[/Vlan x2]/IPv4/TCP
-    // ends at byte 62); deeper chains (tunnels) read the rest through L2.
-    if (w == 0) w = b->offsets ? 64u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
+    // Auto window.  Fixed stride: the slot up to 64 bytes, which hold every header of the common
+    // chains (Ether[/Vlan x2]/IPv4/TCP ends at byte 62).  Indexed batches (pcap replays, tunnels):
+    // 128 bytes from the packet (144 from its 16-byte-aligned start), which hold every header of
+    // the 22 reference templates (the longest chain ends at byte 124), so neither the lockstep walk
+    // nor the field emit goes back to global memory; the loads skip chunks past each packet's end.
+    if (w == 0) w = b->offsets ? 128u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);

@@ -1,13 +1,12 @@
 // pktgpu_device.hpp — device code of the batched parser (gfx950 / CDNA4).
 //
-// One lane per packet, 256-packet blocks.  Each lane loads its packet's first NCH 16-byte chunks
-// with per-lane dwordx4 loads.  Aligned Ether/IPv4/UDP|TCP packets are decoded straight from
-// those registers (RegView, the fast path).  Every other packet's chunks are written to the
-// lane's own LDS window (packet-major, odd dword stride: conflict-free per-lane dword reads) and
-// the lane walks its header chain out of LDS with dword reads at per-lane byte offsets
-// (v_alignbyte for the unaligned part, v_perm for the big-endian swap); a chain that runs past
-// the window falls back to dword loads from global memory.  A lane reads only the LDS it wrote,
-// so there is no barrier.
+// One lane per packet, 256-packet blocks.  The wave loads its packets' first NCH 16-byte chunks
+// cooperatively into each lane's own LDS window (packet-major, odd dword stride: conflict-free
+// per-lane dword reads).  Aligned Ether/0-2 Vlan/IPv4/UDP|TCP packets have their chain decided by a
+// few compares (the fast path); every other lane walks its header chain out of LDS with dword reads
+// at per-lane byte offsets (v_alignbyte for the unaligned part, a byte swap for big-endian); a
+// chain that runs past the window falls back to dword loads from global memory.  No barrier
+// beyond the wave's own: a lane reads only its own window.
 //
 // The walk is the forward, iterative form of the reference's recursion
 // (src/parser/fast.rs:5-227): each step checks the bounds the reference's slice indexing would
@@ -94,12 +93,6 @@ __device__ __forceinline__ uint32_t gre_next(uint32_t p) {
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // A lane's view of its packet: LDS window + global fallback.
-#ifndef PKTGPU_LDS_UNALIGNED
-// hdr<>'s window reads as unaligned LDS loads (gfx950 unaligned-ds-access), not dword pairs +
-// v_alignbyte: C2 isolated 28.9 -> 27.3 us (profiles/ab/r02ulds_unaligned_lds.txt).  le() keeps
-// the dword pair: as one unaligned load it made extract_kernel's 19 getters 68.6 -> 79.5 us.
-#define PKTGPU_LDS_UNALIGNED 1
-#endif
 struct PacketView {
     const uint8_t* lw;        // LDS window of this packet (dword-aligned)
     const uint8_t* slab;      // slab base (16-byte aligned)
@@ -147,20 +140,15 @@ struct PacketView {
         uint32_t a[NW + 1];
         uint32_t sh;
         if (b >= win_lo && b + 4 * NW <= win_end) {
-#if PKTGPU_LDS_UNALIGNED
-            // unaligned LDS reads (gfx950 unaligned-ds-access): the header's bytes as they lie
+            // unaligned LDS reads (gfx950 unaligned-ds-access): the header's bytes as they lie, not
+            // dword pairs + v_alignbyte (C2 isolated 28.9 -> 27.3 us,
+            // profiles/ab/r02ulds_unaligned_lds.txt; le() keeps the dword pair: as one unaligned load
+            // it made extract_kernel's 19 getters 68.6 -> 79.5 us)
             uint32_t u[NW];
             __builtin_memcpy(u, lw + (uint32_t)(b + shift), 4 * NW);
 #pragma unroll
             for (int i = 0; i < NW; i++) d[i] = bswap32(u[i]);
             return;
-#else
-            const uint32_t wb = b + shift;
-            const uint32_t k = wb >> 2;
-            sh = wb & 3;
-#pragma unroll
-            for (int i = 0; i <= NW; i++) a[i] = wdw(k + i);
-#endif
         } else {
             const uint64_t ga = off + b, g4 = ga & ~(uint64_t)3;
             sh = (uint32_t)(ga & 3);
@@ -191,21 +179,6 @@ struct PacketView {
 struct WalkResult {
     uint32_t status, n, payload_off, mask;
     int32_t f_eth, f_vlan, f_ipv4, f_ipv6, f_tcp, f_udp;  // first offsets, -1 = absent
-};
-
-// The first 16*NW bytes of a packet that starts 16-byte aligned, held in registers (little-endian
-// dwords, as loaded).  Same hdr<> interface as PacketView; with a compile-time offset b every
-// index is static, so nothing touches LDS or scratch.
-template <int NW>
-struct RegView {
-    uint32_t w[NW * 4];
-    template <int N>
-    __device__ __forceinline__ void hdr(uint32_t b, uint32_t nbytes, uint32_t (&d)[N]) const {
-        (void)nbytes;
-        const uint32_t k = b >> 2, sh = b & 3u;
-#pragma unroll
-        for (int i = 0; i < N; i++) d[i] = bswap32(__builtin_amdgcn_alignbyte(w[k + i + 1], w[k + i], sh));
-    }
 };
 
 // Header type and size recorded by the walk state S (make_header! sizes, headers.rs:529-827).
@@ -374,22 +347,30 @@ __device__ __forceinline__ uint32_t tab6(uint64_t lo, uint64_t hi, uint32_t st) 
 // early returns: a branchy form made the compiler copy the whole lane state at every exit).  Only
 // GRE options and the ERSPAN3 platform header take a branch, taken when a lane needs it.
 // Semantics are exactly step<S>'s: same checks in the same order, same records.  The first offset
-// of each type 1..7 goes to the lane's LDS slot fl[type * fs] when the type is first recorded.
+// of each field group's type (Ether, Vlan, IPv4, IPv6, TCP, UDP; Q11) is kept in f[] when the type is
+// first recorded.
 struct LockLane {
     uint32_t st, o, n, mask, status, pay, steps;
     bool live;
+    int32_t f[6];  // first offsets of types 1, 2, 3, 4, 6, 7 (-1 = none)
 };
 
 template <class Push>
-__device__ __forceinline__ void lrec(LockLane& L, uint32_t t, uint32_t off, Push& push, uint16_t* fl, uint32_t fs) {
+__device__ __forceinline__ void lrec(LockLane& L, uint32_t t, uint32_t off, Push& push) {
     push(L.n, t, off);
-    if (t <= PKT_HDR_UDP && !((L.mask >> t) & 1u)) fl[t * fs] = (uint16_t)off;
+    const bool first = !((L.mask >> t) & 1u);
+    L.f[0] = (first && t == PKT_HDR_ETHER) ? (int32_t)off : L.f[0];
+    L.f[1] = (first && t == PKT_HDR_VLAN) ? (int32_t)off : L.f[1];
+    L.f[2] = (first && t == PKT_HDR_IPV4) ? (int32_t)off : L.f[2];
+    L.f[3] = (first && t == PKT_HDR_IPV6) ? (int32_t)off : L.f[3];
+    L.f[4] = (first && t == PKT_HDR_TCP) ? (int32_t)off : L.f[4];
+    L.f[5] = (first && t == PKT_HDR_UDP) ? (int32_t)off : L.f[5];
     L.mask |= 1u << t;
     L.n++;
 }
 
 template <class Push>
-__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push, uint16_t* fl, uint32_t fs) {
+__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push) {
     const uint32_t st = L.st, o = L.o;
     L.steps++;
     const uint32_t sz = tab6(kSz0, kSz1, st);
@@ -420,7 +401,7 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
     const bool go = f == 0 && !acc;
     uint32_t q = o;
     if (go && st != S_PARSE) {
-        lrec(L, tab6(kTy0, kTy1, st), o, push, fl, fs);
+        lrec(L, tab6(kTy0, kTy1, st), o, push);
         q = o + sz;
         const bool gopt = st == S_GRE && (D & 0xB0000000u) != 0;
         const bool plat = st == S_ERSPAN3 && (D & 1u);
@@ -436,14 +417,14 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
             const uint32_t oseq = q;
             q += 4u * sb;
             if (!f) {
-                if (sb) lrec(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push, fl, fs);
-                if (k) lrec(L, PKT_HDR_GRE_KEY, okey, push, fl, fs);
-                if (c) lrec(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push, fl, fs);
+                if (sb) lrec(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push);
+                if (k) lrec(L, PKT_HDR_GRE_KEY, okey, push);
+                if (c) lrec(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push);
             }
         } else if (plat) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
             f = (q + 8 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
             if (!f) {
-                lrec(L, PKT_HDR_ERSPAN_PLATFORM, q, push, fl, fs);
+                lrec(L, PKT_HDR_ERSPAN_PLATFORM, q, push);
                 q += 8;
             }
         }
@@ -460,15 +441,15 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
 // layout runs exactly one case per header, a mixed wave one case per distinct (state, depth).
 // WK = 1, lockstep: every live lane advances one header per iteration through lstep() — a mixed
 // wave runs (its longest chain + 2) iterations (C4: 10 instead of ~38).
-// Lockstep extra: fl/fs = the lane's first-offset LDS slots (fl[type * fs]).  (Refilling the
-// window for headers past it, one round trip per wave instead of one dependent read per header,
-// measured slower: C4 status-only 88-90 vs 66-68 us; so did prefetching the sectors past the
-// window into L2, 78 vs 67 us — profiles/ab/r02o_c4_refill_prefetch.txt.)
+// (Refilling the window for headers past it, one round trip per wave instead of one dependent read
+// per header, measured slower: C4 status-only 88-90 vs 66-68 us; so did prefetching the sectors past
+// the window into L2, 78 vs 67 us — profiles/ab/r02o_c4_refill_prefetch.txt.  Round 3 instead sizes
+// indexed windows to hold every header the 22 templates carry, parse_kernel.)
 template <int WK, class Push>
 __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active, Push&& push,
-                                     WalkResult& out, uint16_t* fl = nullptr, uint32_t fs = 0) {
+                                     WalkResult& out) {
     if constexpr (WK == 1) {
-        LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active};
+        LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active, {-1, -1, -1, -1, -1, -1}};
         while (__ballot(L.live)) {
             if (L.live) {
                 // the dispatch dword of this step (big-endian; bytes past the header are read but
@@ -485,20 +466,20 @@ __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active
                 } else if (want) {
                     D = pv.le(b, 4);
                 }
-                lstep(L, pv.len, bswap32(D), push, fl, fs);
+                lstep(L, pv.len, bswap32(D), push);
             }
         }
         out.status = L.status;
         out.n = L.n;
         out.payload_off = L.pay;
         out.mask = L.mask;
-        const uint32_t m = L.status == PKT_OK ? L.mask : 0u;
-        out.f_eth = (m >> PKT_HDR_ETHER) & 1u ? (int32_t)fl[PKT_HDR_ETHER * fs] : -1;
-        out.f_vlan = (m >> PKT_HDR_VLAN) & 1u ? (int32_t)fl[PKT_HDR_VLAN * fs] : -1;
-        out.f_ipv4 = (m >> PKT_HDR_IPV4) & 1u ? (int32_t)fl[PKT_HDR_IPV4 * fs] : -1;
-        out.f_ipv6 = (m >> PKT_HDR_IPV6) & 1u ? (int32_t)fl[PKT_HDR_IPV6 * fs] : -1;
-        out.f_tcp = (m >> PKT_HDR_TCP) & 1u ? (int32_t)fl[PKT_HDR_TCP * fs] : -1;
-        out.f_udp = (m >> PKT_HDR_UDP) & 1u ? (int32_t)fl[PKT_HDR_UDP * fs] : -1;
+        const bool ok = L.status == PKT_OK;
+        out.f_eth = ok ? L.f[0] : -1;
+        out.f_vlan = ok ? L.f[1] : -1;
+        out.f_ipv4 = ok ? L.f[2] : -1;
+        out.f_ipv6 = ok ? L.f[3] : -1;
+        out.f_tcp = ok ? L.f[4] : -1;
+        out.f_udp = ok ? L.f[5] : -1;
         return;
     }
     Lane L;

@@ -12,16 +12,22 @@
 #include <algorithm>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "pktgpu_ctx.hpp"
 
 struct pkt_mgpu {
+    static constexpr int kMaxStreams = 4;
     int ndev = 0;
     std::vector<int> dev;
     std::vector<pkt_ctx_t*> ctx;
-    std::vector<hipStream_t> stream;
+    std::vector<hipStream_t> stream;  // each device's work stream (the gather runs on it)
     std::vector<ncclComm_t> comm;
+    // pkt_mgpu_parse_steps: extra streams per device (joined back into `stream` after each call)
+    // and one event per stream, created on first use
+    std::vector<hipStream_t> xs;  // [ndev][kMaxStreams - 1]
+    std::vector<hipEvent_t> xe;   // [ndev][kMaxStreams]
     std::string err;
 };
 
@@ -209,6 +215,13 @@ int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
     for (int i = 0; i < mg->ndev; i++) {
         (void)hipSetDevice(mg->dev[i]);
         if (mg->stream[i]) (void)hipStreamSynchronize(mg->stream[i]);
+        for (size_t k = i * (pkt_mgpu::kMaxStreams - 1); k < mg->xs.size() && k < (i + 1) * (pkt_mgpu::kMaxStreams - 1ull); k++)
+            if (mg->xs[k]) {
+                (void)hipStreamSynchronize(mg->xs[k]);
+                (void)hipStreamDestroy(mg->xs[k]);
+            }
+        for (size_t k = i * pkt_mgpu::kMaxStreams; k < mg->xe.size() && k < (i + 1) * (size_t)pkt_mgpu::kMaxStreams; k++)
+            if (mg->xe[k]) (void)hipEventDestroy(mg->xe[k]);
         if (mg->comm[i]) (void)ncclCommDestroy(mg->comm[i]);
         if (mg->stream[i]) (void)hipStreamDestroy(mg->stream[i]);
         if (mg->ctx[i]) pkt_ctx_destroy(mg->ctx[i]);
@@ -235,6 +248,73 @@ int pkt_mgpu_parse(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry, uint64
         if (rc != PKT_SUCCESS)
             return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
     }
+    return PKT_SUCCESS;
+}
+
+int pkt_mgpu_parse_steps(pkt_mgpu_t* mg, const pkt_batch_t* batches, int steps, int entry, uint64_t mask,
+                         void* const* shard_out, int streams) {
+    if (!mg || (steps > 0 && (!batches || !shard_out))) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
+    if (steps < 0 || streams < 1 || streams > pkt_mgpu::kMaxStreams)
+        return mfail(mg, PKT_ERR_INVALID_ARG, "steps < 0 or streams not in 1..4");
+    if (mask >> kNumCols) return mfail(mg, PKT_ERR_INVALID_ARG, "bad column mask");
+    const int nd = mg->ndev, S = streams;
+    for (int k = 0; k < steps * nd; k++)
+        if (batches[k].n && !shard_out[k]) return mfail(mg, PKT_ERR_INVALID_ARG, "null shard output");
+    if (mg->xs.empty()) {  // extra streams and the join events, once
+        mg->xs.assign((size_t)nd * (pkt_mgpu::kMaxStreams - 1), nullptr);
+        mg->xe.assign((size_t)nd * pkt_mgpu::kMaxStreams, nullptr);
+        for (int i = 0; i < nd; i++) {
+            hipError_t e = hipSetDevice(mg->dev[i]);
+            for (int j = 0; j < pkt_mgpu::kMaxStreams - 1 && e == hipSuccess; j++)
+                e = hipStreamCreateWithFlags(&mg->xs[i * (pkt_mgpu::kMaxStreams - 1) + j], hipStreamNonBlocking);
+            for (int j = 0; j < pkt_mgpu::kMaxStreams && e == hipSuccess; j++)
+                e = hipEventCreateWithFlags(&mg->xe[i * pkt_mgpu::kMaxStreams + j], hipEventDisableTiming);
+            if (e != hipSuccess) return mhip(mg, e, "pkt_mgpu_parse_steps streams");
+        }
+    }
+    // One host thread per device issues that device's launches (one launch per step, round-robin
+    // over S streams that first wait for the device's work stream and are joined back into it), so
+    // the launch rate grows with the device count instead of serialising on one thread.
+    std::vector<int> rc(nd, PKT_SUCCESS);
+    std::vector<std::string> why(nd);
+    auto issue = [&](int i) {
+        hipError_t e = hipSetDevice(mg->dev[i]);
+        hipStream_t st[pkt_mgpu::kMaxStreams];
+        st[0] = mg->stream[i];
+        for (int j = 1; j < S; j++) st[j] = mg->xs[i * (pkt_mgpu::kMaxStreams - 1) + j - 1];
+        hipEvent_t* ev = &mg->xe[i * pkt_mgpu::kMaxStreams];
+        if (e == hipSuccess && S > 1) e = hipEventRecord(ev[0], st[0]);
+        for (int j = 1; j < S && e == hipSuccess; j++) e = hipStreamWaitEvent(st[j], ev[0], 0);
+        if (e != hipSuccess) {
+            rc[i] = PKT_ERR_HIP;
+            why[i] = std::string("stream setup: ") + hipGetErrorString(e);
+            return;
+        }
+        for (int k = 0; k < steps && rc[i] == PKT_SUCCESS; k++) {
+            pkt_out_t o;
+            pkt_out_packed(mask, batches[k * nd + i].n, shard_out[k * nd + i], &o, nullptr);
+            rc[i] = pkt_parse_batch(mg->ctx[i], &batches[k * nd + i], entry, &o, st[k % S]);
+            if (rc[i] != PKT_SUCCESS) why[i] = pkt_ctx_last_error(mg->ctx[i]);
+        }
+        for (int j = 1; j < S; j++) {  // join (also after a failed launch: the queued ones stay ordered)
+            hipError_t ej = hipEventRecord(ev[j], st[j]);
+            if (ej == hipSuccess) ej = hipStreamWaitEvent(st[0], ev[j], 0);
+            if (ej != hipSuccess && rc[i] == PKT_SUCCESS) {
+                rc[i] = PKT_ERR_HIP;
+                why[i] = std::string("stream join: ") + hipGetErrorString(ej);
+            }
+        }
+    };
+    if (nd == 1) {
+        issue(0);
+    } else {
+        std::vector<std::thread> th;
+        th.reserve(nd);
+        for (int i = 0; i < nd; i++) th.emplace_back(issue, i);
+        for (auto& t : th) t.join();
+    }
+    for (int i = 0; i < nd; i++)
+        if (rc[i] != PKT_SUCCESS) return mfail(mg, rc[i], "shard " + std::to_string(i) + ": " + why[i]);
     return PKT_SUCCESS;
 }
 

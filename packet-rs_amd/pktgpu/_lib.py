@@ -114,6 +114,8 @@ SIGNATURES = {
     "pkt_mgpu_stream": (_P, [_P, ctypes.c_int]),
     "pkt_mgpu_parse": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_uint64,
                                       ctypes.POINTER(_P)]),
+    "pkt_mgpu_parse_steps": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_int,
+                                            ctypes.c_uint64, ctypes.POINTER(_P), ctypes.c_int]),
     "pkt_mgpu_gather": (ctypes.c_int, [_P, ctypes.c_int, ctypes.POINTER(_P), ctypes.POINTER(ctypes.c_uint64),
                                        _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_mgpu_parse_gather": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.c_uint64,

@@ -53,6 +53,18 @@ def packed_bytes(columns, n):
     return nb.value
 
 
+def packed_pieces(columns, n, rows):
+    """(offsets, lengths) of the byte ranges of an n-packet packed buffer holding every column with
+    only the first `rows` slot rows (pkt_out_packed_pieces): what a copy or gather must move."""
+    from . import _lib
+    L = _lib.load()
+    po, pl, npc = (ctypes.c_uint64 * 2)(), (ctypes.c_uint64 * 2)(), ctypes.c_int()
+    if L.pkt_out_packed_pieces(schema.column_mask(resolve_columns(columns)), int(n), int(rows), po, pl,
+                               ctypes.byref(npc)) != 0:
+        raise ValueError("pkt_out_packed_pieces: bad arguments")
+    return [po[k] for k in range(npc.value)], [pl[k] for k in range(npc.value)]
+
+
 def shard_range(n, nshards, i):
     """The library's contiguous split (pkt_shard_range): [lo, hi) of shard i."""
     from . import _lib
@@ -177,6 +189,50 @@ class MultiParser:
             b.stride = stride or 0
             b.n = int(n)
         return arr
+
+    def set_knobs(self, fastpath=None, staging=None, window=None, walk=None):
+        """pkt_ctx_set_* on every device's ctx."""
+        for i in range(self.ndev):
+            c = self.ctx(i)
+            if fastpath is not None:
+                self._check(self._L.pkt_ctx_set_fastpath(c, int(bool(fastpath))), "pkt_ctx_set_fastpath")
+            if staging is not None:
+                self._check(self._L.pkt_ctx_set_staging(c, int(staging)), "pkt_ctx_set_staging")
+            if window is not None:
+                self._check(self._L.pkt_ctx_set_window(c, int(window)), "pkt_ctx_set_window")
+            if walk is not None:
+                self._check(self._L.pkt_ctx_set_walk(c, int(walk)), "pkt_ctx_set_walk")
+
+    def steps_plan(self, steps):
+        """Prebuilt argument arrays of pkt_mgpu_parse_steps for `steps` steps: a list with, per
+        step, one (shard tuple, packed output tensor) per device ->
+        (PktBatch[steps * ndev], void*[steps * ndev]), step-major."""
+        nd = self.ndev
+        b = (self._lib.PktBatch * max(1, len(steps) * nd))()
+        o = (ctypes.c_void_p * max(1, len(steps) * nd))()
+        for k, per_dev in enumerate(steps):
+            assert len(per_dev) == nd
+            one = self._batches([sh for sh, _ in per_dev])
+            for i, (_, out) in enumerate(per_dev):
+                b[k * nd + i] = one[i]
+                o[k * nd + i] = out.data_ptr()
+        return b, o, len(steps)
+
+    def parse_steps(self, plan, entry="parse", columns="all", first=0, count=None, streams=2):
+        """Steps [first, first + count) of a steps_plan in one pkt_mgpu_parse_steps call (one host
+        thread per device issues that device's launches over `streams` streams).  Asynchronous on
+        the handle's streams; no ordering with torch's streams (the bench owns every buffer)."""
+        b, o, n = plan
+        count = n - first if count is None else count
+        assert 0 <= first and first + count <= n
+        nd = self.ndev
+        e = schema.ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        bp = ctypes.cast(ctypes.byref(b, first * nd * ctypes.sizeof(self._lib.PktBatch)),
+                         ctypes.POINTER(self._lib.PktBatch))
+        op = ctypes.cast(ctypes.byref(o, first * nd * ctypes.sizeof(ctypes.c_void_p)), ctypes.POINTER(ctypes.c_void_p))
+        self._check(self._L.pkt_mgpu_parse_steps(self._mg, bp, int(count), e,
+                                                 schema.column_mask(resolve_columns(columns)), op, int(streams)),
+                    "pkt_mgpu_parse_steps")
 
     # ---------------------------------------------------------------- parse + gather
     def alloc_shard_outputs(self, shards, columns):

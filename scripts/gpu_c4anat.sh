@@ -6,7 +6,7 @@ TAG=${1:-r03anat}; OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 P1="TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_READ_sum"
 P2="TCC_HIT_sum TCC_MISS_sum TCC_WRITE_sum TCC_REQ_sum"
-for w in 0 128; do for v in status chain all; do
+for w in ${WINDOWS:-64 0}; do for v in ${VARIANTS:-status all}; do
   for p in 1 2; do
     eval C=\$P$p
     timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $C --output-format csv -d $OUT/w${w}_${v}_p$p -o pmc -- \
@@ -14,10 +14,10 @@ for w in 0 128; do for v in status chain all; do
   done
 done; done
 python - $OUT <<'PY'
-import csv, glob, sys, collections, statistics
+import csv, glob, sys, collections, statistics, os
 d = sys.argv[1]
-for w in (0, 128):
-    for v in ("status", "chain", "all"):
+for w in [int(x) for x in os.environ.get("WINDOWS", "64 0").split()]:
+    for v in os.environ.get("VARIANTS", "status all").split():
         vals = {}
         for p in (1, 2):
             f = glob.glob(f"{d}/w{w}_{v}_p{p}/**/*counter_collection.csv", recursive=True)[0]

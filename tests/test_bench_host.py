@@ -38,3 +38,22 @@ def test_line_bytes_indexed_vs_brute_force():
         span = np.minimum(lens, rng.integers(0, 200, n))
         perm = rng.permutation(n) if rng.integers(0, 2) else np.arange(n)  # any record order
         assert bench.line_bytes(n, None, offs[perm].astype(np.uint64), span[perm]) == brute_lines(offs, span)
+
+
+def test_gpus_beyond_visible_devices_exits_nonzero():
+    """`bench.py --gpus N` with fewer visible devices must fail, in both forms (the
+    pkt_mgpu one-process form and the --per-rank launcher).  This container has no GPU."""
+    import subprocess
+    import sys
+    import pytest
+    torch = pytest.importorskip("torch")
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("two or more devices visible")
+    for extra in ([], ["--per-rank"]):
+        r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
+                            "--warmup", "1", "--no-cpu-baseline"] + extra,
+                           capture_output=True, text=True, timeout=300,
+                           env=dict(os.environ, HIP_VISIBLE_DEVICES=os.environ.get("HIP_VISIBLE_DEVICES", "")))
+        assert r.returncode != 0, (extra, r.stdout[-500:], r.stderr[-500:])
+        assert "device" in r.stderr, r.stderr[-500:]
+        assert not r.stdout.strip(), r.stdout[-500:]

@@ -203,3 +203,26 @@ def test_mgpu_orders_after_torch_stream(MP):
         _compare(got, ref, f"generator -> parse_gather rep {rep}")
     g.close()
     P.close()
+
+
+@pytest.mark.gpu
+def test_bench_mgpu_leg_at_one_device():
+    """bench.py's measured path is the library's multi-device entry
+    (pkt_mgpu_parse_steps + pkt_mgpu_parse_gather); run it at ndev = 1 with small sizes and check the
+    line's shape and that the C5 gather moved only the used slot rows (69 B per C2 packet)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "1", "--steps", "6",
+                        "--warmup", "2", "--no-cpu-baseline", "--no-extra", "--ring-gib", "0.25",
+                        "--total-packets", str(1 << 21)], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 1 and line["value"] > 0 and line["scaling"] == "weak"
+    assert "pkt_mgpu_parse_steps" in line["config"]["launch"]
+    assert line["roofline"]["frac"] > 0
+    g = line["c5"]["gather"]
+    assert g["slot_rows_moved"] == 3
+    assert 69 <= g["bytes_per_pkt_moved"] <= 70, g
