@@ -207,6 +207,29 @@ __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uin
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// Diagnostic build only (-DPKTGPU_STAMPS=1, scripts/gpu_stamps.sh): s_memtime stamps per wave of the
+// parse kernel — start, windows in LDS, walk done, emit issued, stores drained — plus the wave's
+// hardware id, written by lane 0 to a debug buffer no other code reads (pkt_debug_stamps).  In the
+// normal build no stamp executes.
+#ifndef PKTGPU_STAMPS
+#define PKTGPU_STAMPS 0
+#endif
+#if PKTGPU_STAMPS
+__device__ uint64_t* g_pkt_stamps;
+#define PKT_STAMP(k)                                                                          \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        uint64_t t_;                                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        pkt_st[k] = t_;                                                                       \
+    } while (0)
+#else
+#define PKT_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 // Lane t's packet range and its first NCH 16-byte chunks (from the 16-byte-aligned start) by
 // per-lane dwordx4 loads (faster than the LDS-DMA gather, scripts/probe.py).  Chunks past the
 // readable end of the slab (round_up(slab_len, 16)) are clamped to an in-bounds chunk; those
@@ -243,7 +266,7 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
 template <int NCH, uint32_t GM, int WK, bool STAGED = false>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own);
+                                           bool active_own, uint64_t* pkt_st);
 
 // One block = 256 packets, one lane per packet.  (A persistent grid of k blocks per CU striding
 // over the tiles, each lane's loads of its next packet in flight while it parsed the current one,
@@ -256,6 +279,8 @@ template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
 void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
+    PKT_STAMP(0);
     const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
     const bool act = base + threadIdx.x < p.n;
     u32x4 chunk[NCH];
@@ -270,9 +295,8 @@ void parse_kernel(KParams p) {
         // memory (scripts/fetch_calib.py).  Each chunk goes straight into the owning lane's LDS
         // window.  C4 pipelined 78 vs 82 us/step, C2 23.9 vs 25.2, C3 43.3 vs 46.1 against per-lane
         // loads (profiles/ab/r02p_c4_coop_windows.txt, r02x_coop_fixed_stride.txt).
-        // Lockstep (indexed) launches skip the chunks that start past their packet's end: their
-        // 144-byte windows hold every header of the 22 templates, and a short record (Dot3, ARP)
-        // then fetches only its own lines.
+        // Lockstep (indexed) launches skip the chunks that start past their packet's end: a short
+        // record (Dot3, ARP) fetches only its own lines.
         off = 0;
         len = 0;
         if (act) packet_range(p, base + threadIdx.x, off, len);
@@ -299,17 +323,19 @@ void parse_kernel(KParams p) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act);
+        PKT_STAMP(1);
+        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act, pkt_st);
         return;
     }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act);
+    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act, pkt_st);
 }
 
 template <int NCH, uint32_t GM, int WK, bool STAGED>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own) {
+                                           bool active_own, uint64_t* pkt_st) {
+    (void)pkt_st;
     const uint32_t t = threadIdx.x;
     const uint32_t i_own = base + t;
     // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose EtherType chain is
@@ -386,9 +412,25 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     if constexpr (NCH >= 4) {
         if (fast) fast_result(r, fv);
     }
-    if (!active_own) return;
-    emit_chain<GM>(out, i_own, len_own, r);
-    emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+    PKT_STAMP(2);
+    if (active_own) {
+        emit_chain<GM>(out, i_own, len_own, r);
+        emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+    }
+#if PKTGPU_STAMPS
+    PKT_STAMP(3);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PKT_STAMP(4);
+    if ((t & 63u) == 0 && g_pkt_stamps) {
+        uint32_t hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        uint64_t* d = g_pkt_stamps + ((uint64_t)blockIdx.x * kWavesPerBlock + (t >> 6)) * 8u;
+        for (int k = 0; k < 5; k++) d[k] = pkt_st[k];
+        d[5] = hw;
+        d[6] = xcc & 15u;  // s_memtime counts per XCD: stamps compare within one XCD only
+    }
+#endif
 }
 
 // ---- span staging (indexed batches: the records of a pcap lie back to back) ----
@@ -629,6 +671,15 @@ hipError_t max_hdrs_async(pkt_ctx* ctx, const uint8_t* nh, uint64_t n, int w, hi
 
 extern "C" {
 
+#if PKTGPU_STAMPS
+// Diagnostic build only: where the parse kernel writes its per-wave stamps (8 u64 per wave:
+// 5 s_memtime stamps, HW_ID, batch size).  NULL = none.
+int pkt_debug_stamps(void* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pkt_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? PKT_SUCCESS
+                                                                                           : PKT_ERR_HIP;
+}
+#endif
+
 int pkt_chain_max_hdrs(pkt_ctx_t* ctx, const uint8_t* n_hdrs, uint64_t n, uint32_t* max_out, void* stream) {
     if (!ctx || !max_out || (n && !n_hdrs)) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     hipError_t e = hipSetDevice(ctx->device);
@@ -742,12 +793,13 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Window: bytes of each packet staged in LDS.  Fixed stride: the slot (up to 128 B);
     // indexed: 128 B.  Unaligned packet starts need one more chunk.
     uint32_t w = ctx->window;
-    // Auto window.  Fixed stride: the slot up to 64 bytes, which hold every header of the common
-    // chains (Ether[/Vlan x2]/IPv4/TCP ends at byte 62).  Indexed batches (pcap replays, tunnels):
-    // 128 bytes from the packet (144 from its 16-byte-aligned start), which hold every header of
-    // the 22 reference templates (the longest chain ends at byte 124), so neither the lockstep walk
-    // nor the field emit goes back to global memory; the loads skip chunks past each packet's end.
-    if (w == 0) w = b->offsets ? 128u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
+    // Auto window: 64 bytes of the packet (80 from its 16-byte-aligned start for indexed
+    // batches), which hold every header of the common chains (Ether[/Vlan x2]/IPv4/TCP ends at
+    // byte 62); deeper chains (tunnels) read the rest through L2.  A 128-byte window
+    // (pkt_ctx_set_window(ctx, 128): every header of the 22 reference templates in LDS, C4 line
+    // requests 2.28M -> 1.61M per 2^20 records) measured slower: 37.9 KB of LDS per block allows
+    // 4 blocks per CU instead of 7 (C4 pipelined 81 vs 76 us, isolated equal).
+    if (w == 0) w = b->offsets ? 64u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);

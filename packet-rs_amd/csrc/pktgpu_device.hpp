@@ -355,24 +355,22 @@ struct LockLane {
     int32_t f[6];  // first offsets of types 1, 2, 3, 4, 6, 7 (-1 = none)
 };
 
+// Record (t, off) in slot L.n without touching the first offsets: the GRE option and ERSPAN
+// platform types (14-16, 19) are never one of the six field groups.
 template <class Push>
-__device__ __forceinline__ void lrec(LockLane& L, uint32_t t, uint32_t off, Push& push) {
+__device__ __forceinline__ void lrec_opt(LockLane& L, uint32_t t, uint32_t off, Push& push) {
     push(L.n, t, off);
-    const bool first = !((L.mask >> t) & 1u);
-    L.f[0] = (first && t == PKT_HDR_ETHER) ? (int32_t)off : L.f[0];
-    L.f[1] = (first && t == PKT_HDR_VLAN) ? (int32_t)off : L.f[1];
-    L.f[2] = (first && t == PKT_HDR_IPV4) ? (int32_t)off : L.f[2];
-    L.f[3] = (first && t == PKT_HDR_IPV6) ? (int32_t)off : L.f[3];
-    L.f[4] = (first && t == PKT_HDR_TCP) ? (int32_t)off : L.f[4];
-    L.f[5] = (first && t == PKT_HDR_UDP) ? (int32_t)off : L.f[5];
     L.mask |= 1u << t;
     L.n++;
 }
 
+// One lockstep iteration for lane state L and its dispatch dword D (big-endian), `live` = the lane
+// takes part.  Every new value is computed for every lane and committed by selects (only the
+// slot stores and the rare GRE-option / ERSPAN-platform records branch), so the compiler keeps
+// one copy of the lane state instead of re-materialising it at every divergent merge.
 template <class Push>
-__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push) {
+__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push, bool live) {
     const uint32_t st = L.st, o = L.o;
-    L.steps++;
     const uint32_t sz = tab6(kSz0, kSz1, st);
     const uint32_t hw = D >> 16;
     const uint32_t et_next = etype_next(hw);
@@ -391,49 +389,61 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
     nx = (st == S_UDP) ? (hw == 4789u ? S_VXLAN : S_ACCEPT) : nx;
     // the reference's panics in its order: iteration bound (walk), `&arr[0..X::size()]`, depth,
     // parse_mpls_bos's arr[4] (fast.rs:74-83, Q3); accept ends the walk (fast.rs:223-227)
+    const uint32_t steps = L.steps + 1;
     const bool acc = st == S_ACCEPT;
     uint32_t f = 0;
     f = (st == S_MPLS_BOS && o + 5 > len) ? (uint32_t)PKT_TRUNCATED : f;
     f = (st != S_PARSE && L.n >= PKT_MAX_HDRS) ? (uint32_t)PKT_DEPTH_LIMIT : f;
     f = (o + sz > len) ? (uint32_t)PKT_TRUNCATED : f;
     f = acc ? 0u : f;
-    f = (L.steps > PKT_MAX_HDRS + 3) ? (uint32_t)PKT_DEPTH_LIMIT : f;
-    const bool go = f == 0 && !acc;
-    uint32_t q = o;
-    if (go && st != S_PARSE) {
-        lrec(L, tab6(kTy0, kTy1, st), o, push);
-        q = o + sz;
-        const bool gopt = st == S_GRE && (D & 0xB0000000u) != 0;
-        const bool plat = st == S_ERSPAN3 && (D & 1u);
-        if (gopt) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
-            const uint32_t c = D >> 31, k = (D >> 29) & 1u, sb = (D >> 28) & 1u;
-            if (c) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
-            const uint32_t oc = q;
-            q += 4u * c;
-            if (!f && k) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
-            const uint32_t okey = q;
-            q += 4u * k;
-            if (!f && sb) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c + k >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
-            const uint32_t oseq = q;
-            q += 4u * sb;
-            if (!f) {
-                if (sb) lrec(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push);
-                if (k) lrec(L, PKT_HDR_GRE_KEY, okey, push);
-                if (c) lrec(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push);
-            }
-        } else if (plat) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
-            f = (q + 8 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
-            if (!f) {
-                lrec(L, PKT_HDR_ERSPAN_PLATFORM, q, push);
-                q += 8;
-            }
+    f = (steps > PKT_MAX_HDRS + 3) ? (uint32_t)PKT_DEPTH_LIMIT : f;
+    const bool go = live && f == 0 && !acc;
+    const bool rec = go && st != S_PARSE;
+    // the record of this step's header (branch-free; the slot stores are masked by `rec`)
+    const uint32_t t = tab6(kTy0, kTy1, st);
+    if (rec) push(L.n, t, o);
+    const bool first = rec && !((L.mask >> t) & 1u);
+    L.f[0] = (first && t == PKT_HDR_ETHER) ? (int32_t)o : L.f[0];
+    L.f[1] = (first && t == PKT_HDR_VLAN) ? (int32_t)o : L.f[1];
+    L.f[2] = (first && t == PKT_HDR_IPV4) ? (int32_t)o : L.f[2];
+    L.f[3] = (first && t == PKT_HDR_IPV6) ? (int32_t)o : L.f[3];
+    L.f[4] = (first && t == PKT_HDR_TCP) ? (int32_t)o : L.f[4];
+    L.f[5] = (first && t == PKT_HDR_UDP) ? (int32_t)o : L.f[5];
+    L.mask = rec ? (L.mask | (1u << t)) : L.mask;
+    L.n = rec ? L.n + 1 : L.n;
+    uint32_t q = rec ? o + sz : o;
+    const bool gopt = rec && st == S_GRE && (D & 0xB0000000u) != 0;
+    const bool plat = rec && st == S_ERSPAN3 && (D & 1u);
+    if (gopt) {  // fast.rs:114-165: options sliced C,K,S; listed S,K,C (Q2)
+        const uint32_t c = D >> 31, k = (D >> 29) & 1u, sb = (D >> 28) & 1u;
+        if (c) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+        const uint32_t oc = q;
+        q += 4u * c;
+        if (!f && k) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+        const uint32_t okey = q;
+        q += 4u * k;
+        if (!f && sb) f = (q + 4 > len) ? (uint32_t)PKT_TRUNCATED : (L.n + c + k >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+        const uint32_t oseq = q;
+        q += 4u * sb;
+        if (!f) {
+            if (sb) lrec_opt(L, PKT_HDR_GRE_SEQUENCE_NUM, oseq, push);
+            if (k) lrec_opt(L, PKT_HDR_GRE_KEY, okey, push);
+            if (c) lrec_opt(L, PKT_HDR_GRE_CHKSUM_OFFSET, oc, push);
+        }
+    } else if (plat) {  // fast.rs:172-192: o bit -> ERSPANPLATFORM
+        f = (q + 8 > len) ? (uint32_t)PKT_TRUNCATED : (L.n >= PKT_MAX_HDRS ? (uint32_t)PKT_DEPTH_LIMIT : 0u);
+        if (!f) {
+            lrec_opt(L, PKT_HDR_ERSPAN_PLATFORM, q, push);
+            q += 8;
         }
     }
-    L.pay = (acc && f == 0) ? o : L.pay;
-    L.status = f ? f : L.status;
+    // commit (lanes not taking part keep their state)
+    L.steps = live ? steps : L.steps;
+    L.pay = (live && acc && f == 0) ? o : L.pay;
+    L.status = (live && f) ? f : L.status;
     L.live = go && f == 0;
-    L.o = q;
-    L.st = nx;
+    L.o = live ? q : L.o;
+    L.st = live ? nx : L.st;
 }
 
 // The walk.  WK = 0, waterfall: each iteration takes the state of the first live lane and every
@@ -450,24 +460,23 @@ __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active
                                      WalkResult& out) {
     if constexpr (WK == 1) {
         LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active, {-1, -1, -1, -1, -1, -1}};
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(pv.lw);
         while (__ballot(L.live)) {
-            if (L.live) {
-                // the dispatch dword of this step (big-endian; bytes past the header are read but
-                // never used): from the window when it holds it, else from global memory — and
-                // only if the step gets past its iteration and slice checks
-                const uint32_t b = L.o + tab6(kDw0, kDw1, L.st);
-                const bool want = L.st != S_ACCEPT && L.steps < PKT_MAX_HDRS + 3 &&
-                                  L.o + tab6(kSz0, kSz1, L.st) <= pv.len;
-                uint32_t D = 0;
-                if (b >= pv.win_lo && b + 4 <= pv.win_end) {
-                    const uint32_t wb = b + pv.shift, k = wb >> 2, sh = wb & 3;
-                    const uint32_t* w = reinterpret_cast<const uint32_t*>(pv.lw);
-                    D = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-                } else if (want) {
-                    D = pv.le(b, 4);
-                }
-                lstep(L, pv.len, bswap32(D), push);
+            const bool live = L.live;
+            // the dispatch dword of this step (big-endian; bytes past the header are read but
+            // never used): from the window when it holds it (every lane reads, at an in-window
+            // address), else from global memory — only if the step gets past its iteration and
+            // slice checks (a rare divergent branch)
+            const uint32_t b = L.o + tab6(kDw0, kDw1, L.st);
+            const bool in_win = b >= pv.win_lo && b + 4 <= pv.win_end;
+            const uint32_t wb = in_win ? b + pv.shift : 0u, k = wb >> 2, sh = wb & 3;
+            uint32_t D = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
+            const bool far = live && !in_win && L.st != S_ACCEPT && L.steps < PKT_MAX_HDRS + 3 &&
+                             L.o + tab6(kSz0, kSz1, L.st) <= pv.len;
+            if (__ballot(far)) {
+                if (far) D = pv.le(b, 4);
             }
+            lstep(L, pv.len, bswap32(D), push, live);
         }
         out.status = L.status;
         out.n = L.n;

@@ -59,6 +59,9 @@ constexpr int kHops[2] = {PKTGPU_PCAP_HOPS};
 constexpr int kMinHops = kHops[0], kMaxHops = kHops[1];  // guess chain length
 constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec within a day
 constexpr uint32_t kPassSlots = 64;               // passes with their own control words
+// Repair rounds per pass: 2.  With 1, the C4 capture's first pass always still finds a guess to fix
+// and needs a second pass (one more read-back): 141 vs 111 us per call (round 3, same box).
+constexpr uint32_t kRounds = 2;
 
 // Control words (device, zeroed once per call): [0] magic is d4 c3 b2 a1; then per pass p (slot
 // p % 64): [8 + 8s + 2r] regions that disagreed in round r, [9 + 8s + 2r] K - first such region
@@ -195,16 +198,45 @@ __device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t ba
 }
 
 // Walk the records from `entry` while they start inside the region [base, base + kRegion) and
-// 16 header bytes remain: pkt_pcap_index's loop restated per region.  Every lane walks (LDS
-// broadcast reads at `lbase`-relative offsets); lane 0 writes each record's region offset to
-// `list`.  (Measured: moving the walk to SGPRs, or to 32-bit offsets, was slower on MI355X.)
+// 16 header bytes remain: pkt_pcap_index's loop restated per region.  Record i's offset in the
+// region is kept by lane i in `rec` (a select per record, no branch, no LDS write); records 64..
+// (regions of short records) go to `list` from lane 0.  The position lives in an SGPR
+// (readfirstlane of each LDS read), so the loop's bounds checks are SALU compares and its branches
+// uniform (round 3: guess kernel + 2 repair rounds + scan + emit 111-114 -> 101-102 us per
+// 2^20-record call; the round-1 SGPR walk kept 64-bit positions and measured slower), with 32-bit
+// offsets from lbase while the file's end is < 4 GiB past it; otherwise the 64-bit vector form.
 __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_t* list, uint64_t base,
-                                     uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err) {
+                                     uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err,
+                                     uint32_t& rec) {
+    if (len - lbase <= 0xFFFFFFF0ull) {
+        const uint32_t lane = lane_id();
+        const uint32_t rb = (uint32_t)(base - lbase), rend = rb + kRegion, rlen = (uint32_t)(len - lbase);
+        uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(entry - lbase));
+        uint32_t c = 0, e = 0, rv = 0;
+        while (p < rend && p + 16 <= rlen) {
+            const uint32_t incl = __builtin_amdgcn_readfirstlane(ld32(lw, p + 8));
+            if (incl > rlen - p - 16) {  // pkt_pcap_index: record runs past the end
+                e = 1;
+                p = rlen;
+                break;
+            }
+            rv = lane == c ? p - rb : rv;
+            if (c >= 64u && lane == 0) list[c] = (uint16_t)(p - rb);
+            c++;
+            p += 16 + incl;
+        }
+        exit = lbase + p;
+        cnt = c;
+        err = e;
+        rec = rv;
+        return;
+    }
     uint64_t pos = entry;
     cnt = 0;
     err = 0;
+    rec = 0;
     const uint64_t end = base + kRegion;
-    const bool l0 = lane_id() == 0;
+    const uint32_t lane = lane_id();
     while (pos < end && pos + 16 <= len) {
         const uint32_t incl = ld32(lw, (uint32_t)(pos - lbase) + 8);
         if (pos + 16 + (uint64_t)incl > len) {  // pkt_pcap_index: record runs past the end
@@ -212,18 +244,23 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
             pos = len;
             break;
         }
-        if (l0) list[cnt] = (uint16_t)(pos - base);
+        const uint32_t ro = (uint32_t)(pos - base);
+        rec = lane == cnt ? ro : rec;
+        if (__builtin_amdgcn_readfirstlane(cnt) >= 64u && lane == 0) list[cnt] = (uint16_t)ro;
         cnt++;
         pos += 16 + (uint64_t)incl;
     }
     exit = pos;
 }
 
-// Write a walked region back: the list (coalesced from LDS) and the region's words.
-__device__ __forceinline__ void store_region(const Scratch& S, uint32_t k, const uint16_t* list,
+// Write a walked region back: the record offsets (lane i's register for record i < 64, the LDS
+// list beyond) and the region's words.
+__device__ __forceinline__ void store_region(const Scratch& S, uint32_t k, const uint16_t* list, uint32_t rec,
                                              uint64_t entry, uint64_t exit, uint32_t cnt, uint32_t err) {
     const uint32_t lane = lane_id();
-    for (uint32_t i = lane; i < cnt; i += 64) S.list[(uint64_t)k * kMaxRec + i] = list[i];
+    uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+    if (lane < cnt) dst[lane] = (uint16_t)rec;
+    for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = list[i];
     if (lane == 0) {
         S.entry[k] = entry;
         S.exit[k] = exit;
@@ -232,8 +269,32 @@ __device__ __forceinline__ void store_region(const Scratch& S, uint32_t k, const
     }
 }
 
+// Diagnostic build only (-DPKTGPU_STAMPS=1): s_memtime stamps per guess wave — start, staged,
+// entry found, walked, stored — to a debug buffer no other code reads (pkt_debug_pcap_stamps).
+#ifndef PKTGPU_STAMPS
+#define PKTGPU_STAMPS 0
+#endif
+#if PKTGPU_STAMPS
+__device__ uint64_t* g_pcap_stamps;
+#define PCAP_STAMP(k)                                                                         \
+    do {                                                                                      \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        uint64_t t_;                                                                          \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
+        __builtin_amdgcn_sched_barrier(0);                                                    \
+        pst[k] = t_;                                                                          \
+    } while (0)
+#else
+#define PCAP_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
+
 __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len,
                                                          uint32_t K, Scratch S) {
+    uint64_t pst[5] = {0, 0, 0, 0, 0};
+    (void)pst;
+    PCAP_STAMP(0);
     __shared__ uint4 lds[kBlockBytes / 16 + 2];
     __shared__ uint16_t lst[kWaves][kMaxRec];
     const uint32_t w = threadIdx.x / 64, lane = lane_id();
@@ -245,6 +306,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     if (blockIdx.x == 0)
         for (uint32_t c = 1 + threadIdx.x; c < kCtlWords; c += 256) S.ctl[c] = 0;
     __syncthreads();
+    PCAP_STAMP(1);
     if (k >= K) return;
     if (lane == 0) S.own[k] = 0;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
@@ -275,11 +337,23 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             }
         }
     }
+    PCAP_STAMP(2);
     uint64_t exit;
-    uint32_t cnt, err;
-    walk(lw, lbase, list, base, entry, len, exit, cnt, err);
+    uint32_t cnt, err, rec;
+    walk(lw, lbase, list, base, entry, len, exit, cnt, err, rec);
     wave_lds_sync();
-    store_region(S, k, list, entry, exit, cnt, err);
+    PCAP_STAMP(3);
+    store_region(S, k, list, rec, entry, exit, cnt, err);
+#if PKTGPU_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PCAP_STAMP(4);
+    if (lane == 0 && g_pcap_stamps) {
+        uint32_t xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        for (int q = 0; q < 5; q++) g_pcap_stamps[(uint64_t)k * 8 + q] = pst[q];
+        g_pcap_stamps[(uint64_t)k * 8 + 6] = xcc & 15u;  // s_memtime counts per XCD
+    }
+#endif
 }
 
 // One repair round (see the file header).  `slot` = this round's two control words.
@@ -323,10 +397,10 @@ __global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restr
             if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane_id());
             wave_lds_sync();
             uint64_t exit;
-            uint32_t cnt, err;
-            walk(lw, base, lst[w], base, e, len, exit, cnt, err);
+            uint32_t cnt, err, rec;
+            walk(lw, base, lst[w], base, e, len, exit, cnt, err, rec);
             wave_lds_sync();
-            store_region(S, r, lst[w], e, exit, cnt, err);
+            store_region(S, r, lst[w], rec, e, exit, cnt, err);
             e = exit;
             if (++r >= K || e == S.entry[r] || e < (uint64_t)r * kRegion) break;
         }
@@ -440,6 +514,14 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
 }  // namespace
 
 extern "C" {
+#if PKTGPU_STAMPS
+// Diagnostic build only: where pcap_guess_kernel writes its per-wave stamps (8 u64 per region).
+int pkt_debug_pcap_stamps(void* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pcap_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? PKT_SUCCESS
+                                                                                            : PKT_ERR_HIP;
+}
+#endif
+
 int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                           uint64_t cap, uint64_t* n_out, void* stream) {
     if (!ctx || !buf || !n_out || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
@@ -506,9 +588,9 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
             e = hipMemsetAsync(S.ctl + 8, 0, 8ull * (kCtlWords - 8), s);
             if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
         }
-        for (uint32_t r = 0; r < 2; r++)  // round ids 1, 2, 3, ... (owner words start at 0)
+        for (uint32_t r = 0; r < kRounds; r++)  // round ids 1, 2, 3, ... (owner words start at 0)
             hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r,
-                               2 * pass + r + 1);
+                               kRounds * pass + r + 1);
         hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4);
         if (cap)
             hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap,
@@ -518,7 +600,7 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
         if (e == hipSuccess) e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
         if (!pc.ctl[0]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
-        if (pc.ctl[slot + 2] == 0) {
+        if (pc.ctl[slot + 2 * (kRounds - 1)] == 0) {
             if (pc.ctl[slot + 4]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
             *n_out = pc.ctl[slot + 5];
             return PKT_SUCCESS;
