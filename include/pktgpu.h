@@ -259,8 +259,9 @@ int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
 /* Tuning knob: how packet bytes reach LDS.  0 = automatic (currently 1), 1 = per-lane windows of
  * pkt_ctx_set_window bytes (deeper headers read through L2), 2 = wave spans: each wave of 64
  * packets copies the contiguous byte range its packets occupy (up to 16 KiB; else per-lane
- * windows) into LDS by LDS-DMA and walks every header from there.
- * Results are identical in every mode. */
+ * windows) into LDS by LDS-DMA and walks every header from there, 3 = pipelined windows (windows
+ * of >= 64 bytes): persistent waves, each loading its next tile's windows while it walks the
+ * current one.  Results are identical in every mode. */
 int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 
 /* Tuning knob: walk schedule.  0 = automatic (lockstep for indexed batches, waterfall for fixed

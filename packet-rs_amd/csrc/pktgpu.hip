@@ -523,11 +523,111 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
 }
 
 
-// How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
-enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
+// ---- pipelined windows (pkt_ctx_set_staging 3): persistent waves, the next tile's windows in
+// flight while the current tile is walked ----
+// A wave walks tile t out of LDS while the cooperative loads of its next tile t + W (W = waves in
+// the grid) land in registers, and the packet ranges of tile t + 2W are loaded one iteration ahead
+// of those, so every wave always has memory in flight: the wide windows (all headers of the
+// templates in LDS, no dependent global read in the walk or the emit) cost LDS per wave, and the
+// waves the LDS allows must not sit idle during their loads.
+template <int NCH>
+__device__ __forceinline__ void tile_range(const KParams& p, uint32_t tile, uint32_t wl, uint64_t& off, uint32_t& len) {
+    off = 0;
+    len = 0;
+    const uint32_t i = tile * 64u + wl;
+    if (i < p.n) packet_range(p, i, off, len);
+}
+
+template <int NCH>
+__device__ __forceinline__ void tile_chunks(const KParams& p, uint32_t wl, uint64_t off, uint32_t len,
+                                            u32x4 (&ch)[NCH]) {
+    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
+        const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
+        const uint32_t lenr = (uint32_t)__shfl((int)len, (int)r, 64);
+        uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
+        a = a > last16 ? last16 : a;
+        ch[k] = u32x4{0, 0, 0, 0};
+        if (16u * c < (uint32_t)(offr & 15) + lenr) ch[k] = *reinterpret_cast<const u32x4*>(p.slab + a);
+    }
+}
+
+template <int NCH>
+__device__ __forceinline__ void tile_stage(uint8_t* lds, uint32_t wl, uint32_t wave0, const u32x4 (&ch)[NCH]) {
+#pragma unroll
+    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
+        const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
+        uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
+        w[0] = ch[k].x;
+        w[1] = ch[k].y;
+        w[2] = ch[k].z;
+        w[3] = ch[k].w;
+    }
+}
+
+// resident waves per SIMD the pipelined kernel is compiled for (VGPRs hold the next tile's chunks)
+__host__ __device__ constexpr int pipe_waves_per_eu(int nch) { return nch >= 9 ? 4 : 6; }
+template <int NCH, uint32_t GM, int WK>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu(NCH))))
+void parse_pipe_kernel(KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
+    const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
+    const uint32_t ntiles = (p.n + 63u) / 64u;
+    const uint32_t W = gridDim.x * (uint32_t)kWavesPerBlock;
+    uint32_t tile = blockIdx.x * (uint32_t)kWavesPerBlock + (threadIdx.x >> 6);  // wave-uniform
+    uint64_t off, off1, off2;
+    uint32_t len, len1, len2;
+    u32x4 ch[NCH];
+    tile_range<NCH>(p, tile, wl, off, len);
+    tile_chunks<NCH>(p, wl, off, len, ch);
+    tile_range<NCH>(p, tile + W, wl, off1, len1);
+    const u32x4 none[NCH] = {};
+    (void)none;
+    while (tile < ntiles) {
+        // this tile's chunks into the lanes' windows (the previous tile's walk and emit are done)
+        __builtin_amdgcn_wave_barrier();
+        tile_stage<NCH>(lds, wl, wave0, ch);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // the next tile's loads in flight (chunks of tile + W, ranges of tile + 2W)
+        if (tile + W < ntiles) tile_chunks<NCH>(p, wl, off1, len1, ch);
+        tile_range<NCH>(p, tile + 2 * W, wl, off2, len2);
+        // walk and emit this tile from LDS
+        const uint32_t base = tile * 64u - wave0;  // parse_tile's lane index = base + threadIdx.x
+        parse_tile<NCH, GM, WK, true>(p, lds, base, none, off, len, tile * 64u + wl < p.n, pkt_st);
+        off = off1;
+        len = len1;
+        off1 = off2;
+        len1 = len2;
+        tile += W;
+    }
+}
+
+// How a launch stages packet bytes: per-lane windows (one tile per block), wave spans, or
+// pipelined windows (persistent waves).
+enum LaunchMode { M_TILE = 0, M_SPAN = 2, M_PIPE = 3 };
 
 template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
+    if constexpr (NCH == 4 || NCH == 5 || NCH == 9) if (mode == M_PIPE) {
+        // persistent: as many blocks as reside on a CU (its LDS over the block's windows, and the
+        // waves per SIMD the kernel is compiled for), at most one wave per tile
+        int cus = 256, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t per_cu = std::max<uint32_t>(
+            1u, std::min<uint32_t>((uint32_t)((160u * 1024u) / window_lds(NCH)),
+                                   (uint32_t)(4 * pipe_waves_per_eu(NCH) / kWavesPerBlock)));
+        const uint32_t tiles = (kp.n + 63u) / 64u;
+        const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus * per_cu, (tiles + kWavesPerBlock - 1) / kWavesPerBlock));
+        hipLaunchKernelGGL((parse_pipe_kernel<NCH, GM, WK>), dim3(blocks), dim3(kBlock), window_lds(NCH), s, kp);
+        return hipGetLastError();
+    }
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), span_region(NCH), s, kp);
@@ -753,7 +853,7 @@ int pkt_ctx_set_fastpath(pkt_ctx_t* ctx, int enable) {
 }
 
 int pkt_ctx_set_staging(pkt_ctx_t* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 3) return PKT_ERR_INVALID_ARG;
     ctx->staging = mode;
     return PKT_SUCCESS;
 }
@@ -810,7 +910,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // Staging: wave spans when asked; per-lane windows otherwise (auto: spans measured slower on
     // device-resident C3 and C4).
-    const int mode = staging == 2 ? M_SPAN : M_TILE;
+    const int mode = staging == 2 ? M_SPAN : (staging == 3 ? M_PIPE : M_TILE);
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
@@ -833,12 +933,11 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
+        // compiled window widths (chunks): a request between two is served by the wider one
         if (nch <= 2) e = launch_gm<2>(kp, gm, mode, wk, s);
         else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, wk, s);
         else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, wk, s);
-        else if (nch <= 8) e = launch_gm<8>(kp, gm, mode, wk, s);
         else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, wk, s);
-        else if (nch <= 16) e = launch_gm<16>(kp, gm, mode, wk, s);
         else e = launch_gm<17>(kp, gm, mode, wk, s);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");

@@ -25,7 +25,8 @@ struct HostPipe {
 struct PcapScratch {
     void* buf = nullptr;   // regions x (entry u64, exit u64, count u32, err u32) + record lists + scan
     uint64_t bytes = 0;
-    uint64_t* ctl = nullptr;  // pinned host words the indexer reads back (change count, totals)
+    uint64_t* ctl = nullptr;      // pinned host words the indexer reads back (change count, totals)
+    uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the scan kernel writes them)
 };
 
 // Element size of each pkt_out_t column, in declaration order (slot columns: one slot; the

@@ -34,6 +34,7 @@
 // HBM traffic ≈ the file once + 2 B/record (the list) written and read + 12 B/record of output.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "pktgpu_ctx.hpp"
@@ -290,27 +291,34 @@ __device__ uint64_t* g_pcap_stamps;
     } while (0)
 #endif
 
-__global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len,
-                                                         uint32_t K, Scratch S) {
-    uint64_t pst[5] = {0, 0, 0, 0, 0};
+// Stage in two halves: the loads (all in flight together) into registers, later the LDS writes —
+// so the next tile's bytes can be in flight while the current tile is walked.
+constexpr uint32_t kStagePieces = kBlockBytes / 16 + 2, kStagePer = (kStagePieces + 255) / 256;
+__device__ __forceinline__ void stage_load(uint4 (&v)[kStagePer], const uint8_t* buf, uint64_t base, uint64_t len,
+                                           uint32_t t) {
+#pragma unroll
+    for (uint32_t i = 0; i < kStagePer; i++) {
+        const uint32_t q = t + i * 256;
+        const uint64_t a = base + 16ull * q;
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (q <= kBlockBytes / 16 && a < len) v[i] = *reinterpret_cast<const uint4*>(buf + a);
+    }
+}
+__device__ __forceinline__ void stage_store(uint4* l4, const uint4 (&v)[kStagePer], uint32_t t) {
+#pragma unroll
+    for (uint32_t i = 0; i < kStagePer; i++)
+        if (t + i * 256 < kStagePieces) l4[t + i * 256] = v[i];
+}
+
+// One region's guess (wave w of the block whose 4 regions are staged at lbase): its entry by the
+// candidate scan, then its walk, stored to the region's words and list.
+__device__ __forceinline__ void guess_region(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K, const Scratch& S,
+                                             const uint32_t* lw, uint16_t* list, uint64_t lbase, uint32_t k,
+                                             uint64_t* pst) {
     (void)pst;
-    PCAP_STAMP(0);
-    __shared__ uint4 lds[kBlockBytes / 16 + 2];
-    __shared__ uint16_t lst[kWaves][kMaxRec];
-    const uint32_t w = threadIdx.x / 64, lane = lane_id();
-    const uint32_t k = blockIdx.x * kWaves + w;
-    const uint64_t lbase = (uint64_t)blockIdx.x * kBlockBytes, lend = lbase + kBlockBytes;
-    stage<kBlockBytes, 256>(lds, buf, lbase, len, threadIdx.x);
-    // the per-call zeroing the repair rounds rely on (no memset launches): control words 1.. here,
-    // word 0 (the magic) and each region's owner word below
-    if (blockIdx.x == 0)
-        for (uint32_t c = 1 + threadIdx.x; c < kCtlWords; c += 256) S.ctl[c] = 0;
-    __syncthreads();
-    PCAP_STAMP(1);
-    if (k >= K) return;
+    const uint32_t lane = lane_id();
+    const uint64_t lend = lbase + kBlockBytes;
     if (lane == 0) S.own[k] = 0;
-    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
-    uint16_t* list = lst[w];
     const uint64_t base = (uint64_t)k * kRegion;
     uint64_t entry = 24;
     if (k == 0) {
@@ -354,6 +362,38 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         g_pcap_stamps[(uint64_t)k * 8 + 6] = xcc & 15u;  // s_memtime counts per XCD
     }
 #endif
+}
+
+// Persistent blocks, each looping over block tiles (4 consecutive regions = 16 KiB): the next
+// tile's 16 KiB are loaded into registers while the current tile's regions are scanned and walked
+// out of LDS, so staging the file overlaps the sequential walks.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(6))) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len,
+                                                         uint32_t K, Scratch S) {
+    uint64_t pst[5] = {0, 0, 0, 0, 0};
+    __shared__ uint4 lds[kBlockBytes / 16 + 2];
+    __shared__ uint16_t lst[kWaves][kMaxRec];
+    const uint32_t t = threadIdx.x, w = t / 64;
+    const uint32_t nt = (K + kWaves - 1) / kWaves;  // block tiles
+    // the per-call zeroing the repair rounds rely on (no memset launches): control words 1.. here,
+    // word 0 (the magic) and each region's owner word in guess_region
+    if (blockIdx.x == 0)
+        for (uint32_t c = 1 + t; c < kCtlWords; c += 256) S.ctl[c] = 0;
+    uint32_t T = blockIdx.x;
+    uint4 v[kStagePer];
+    if (T < nt) stage_load(v, buf, (uint64_t)T * kBlockBytes, len, t);
+    while (T < nt) {  // block-uniform
+        PCAP_STAMP(0);
+        __syncthreads();  // the previous tile's regions are done with the LDS
+        stage_store(lds, v, t);
+        __syncthreads();
+        PCAP_STAMP(1);
+        const uint32_t Tn = T + gridDim.x;
+        if (Tn < nt) stage_load(v, buf, (uint64_t)Tn * kBlockBytes, len, t);
+        const uint32_t k = T * kWaves + w;
+        if (k < K)
+            guess_region(buf, len, K, S, reinterpret_cast<const uint32_t*>(lds), lst[w], (uint64_t)T * kBlockBytes, k, pst);
+        T = Tn;
+    }
 }
 
 // One repair round (see the file header).  `slot` = this round's two control words.
@@ -411,7 +451,8 @@ __global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restr
 // totals to bpre, and the OR of the regions' error flags.  The last block to finish (ticket in
 // ctl[slot + 2]) then scans the block totals in place and writes the record total to
 // ctl[slot + 1]; ctl[slot] collects the error flags.
-__global__ __launch_bounds__(256) void pcap_scan_kernel(uint32_t K, uint32_t nb, Scratch S, uint32_t slot) {
+__global__ __launch_bounds__(256) void pcap_scan_kernel(uint32_t K, uint32_t nb, Scratch S, uint32_t slot,
+                                                        uint32_t pass_slot, uint64_t* host_ctl) {
     __shared__ uint64_t wsum[4];
     __shared__ uint64_t carry;
     __shared__ uint32_t last;
@@ -471,6 +512,14 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(uint32_t K, uint32_t nb,
         __syncthreads();
     }
     if (t == 0) S.ctl[slot + 1] = carry;
+    // The pass's verdict to the host's pinned words directly (no copy launch): the magic word and
+    // the pass's 8 control words (the repair rounds' counts, this kernel's error flag and total).
+    __syncthreads();
+    if (t < 9) {
+        const uint32_t wi = t == 0 ? 0u : pass_slot + t - 1;
+        const uint64_t v = wi == slot + 1 ? carry : __hip_atomic_load(&S.ctl[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&host_ctl[wi], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 // 256 threads write the records of kEmitRegions consecutive regions, one record per thread per
@@ -550,7 +599,8 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
         pc.bytes = need + need / 4;
     }
     if (!pc.ctl) {
-        e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kCtlWords, hipHostMallocDefault);
+        e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kCtlWords, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&pc.ctl_dev), pc.ctl, 0);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc (pcap index)");
     }
     Scratch S;
@@ -575,7 +625,13 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
 
     const dim3 blk(256);
     // (the guess kernel zeroes the control words and the owner words)
-    hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
+    {  // persistent: the blocks that reside at once (7 per CU: 70 VGPRs, 18.4 KB of LDS each), at most one per block tile
+        int cus = 256, dev = 0;
+        (void)hipGetDevice(&dev);
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        const uint32_t nt = (K + kWaves - 1) / kWaves;
+        hipLaunchKernelGGL(pcap_guess_kernel, dim3(std::min<uint32_t>(nt, (uint32_t)cus * 7u)), blk, 0, s, buf, len, K, S);
+    }
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap guess launch");
     // Each pass: two repair rounds, then the scan and the emit on speculation, and ONE read-back.
     // When the second round found no region disagreeing, the state it saw was the fixed point and
@@ -591,13 +647,12 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
         for (uint32_t r = 0; r < kRounds; r++)  // round ids 1, 2, 3, ... (owner words start at 0)
             hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r,
                                kRounds * pass + r + 1);
-        hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4);
+        hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4, slot, pc.ctl_dev);
         if (cap)
             hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap,
                                S, offsets, lens);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
-        e = hipMemcpyAsync(pc.ctl, S.ctl, 8ull * (slot + 8), hipMemcpyDeviceToHost, s);
-        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
         if (!pc.ctl[0]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
         if (pc.ctl[slot + 2 * (kRounds - 1)] == 0) {

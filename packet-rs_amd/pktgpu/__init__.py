@@ -104,7 +104,7 @@ class Parser:
         self._check(self._L.pkt_ctx_set_fastpath(self._ctx, int(bool(enable))), "pkt_ctx_set_fastpath")
 
     def set_staging(self, mode):
-        """0 = auto, 1 = per-lane windows, 2 = wave spans (pkt_ctx_set_staging)."""
+        """0 = auto, 1 = per-lane windows, 2 = wave spans, 3 = pipelined windows (pkt_ctx_set_staging)."""
         self._check(self._L.pkt_ctx_set_staging(self._ctx, int(mode)), "pkt_ctx_set_staging")
 
     def set_walk(self, mode):

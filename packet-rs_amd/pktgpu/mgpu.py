@@ -218,10 +218,12 @@ class MultiParser:
                 o[k * nd + i] = out.data_ptr()
         return b, o, len(steps)
 
-    def parse_steps(self, plan, entry="parse", columns="all", first=0, count=None, streams=2):
-        """Steps [first, first + count) of a steps_plan in one pkt_mgpu_parse_steps call (one host
-        thread per device issues that device's launches over `streams` streams).  Asynchronous on
-        the handle's streams; no ordering with torch's streams (the bench owns every buffer)."""
+    def steps_call(self, plan, entry="parse", columns="all", first=0, count=None, streams=2):
+        """A zero-argument callable issuing steps [first, first + count) of a steps_plan through ONE
+        pkt_mgpu_parse_steps call (one host thread per device issues that device's launches over
+        `streams` streams), with every ctypes argument built here: calling it costs one foreign
+        call (the bench's timed region).  Asynchronous on the handle's streams; no ordering with
+        torch's streams (the caller owns every buffer)."""
         b, o, n = plan
         count = n - first if count is None else count
         assert 0 <= first and first + count <= n
@@ -230,9 +232,19 @@ class MultiParser:
         bp = ctypes.cast(ctypes.byref(b, first * nd * ctypes.sizeof(self._lib.PktBatch)),
                          ctypes.POINTER(self._lib.PktBatch))
         op = ctypes.cast(ctypes.byref(o, first * nd * ctypes.sizeof(ctypes.c_void_p)), ctypes.POINTER(ctypes.c_void_p))
-        self._check(self._L.pkt_mgpu_parse_steps(self._mg, bp, int(count), e,
-                                                 schema.column_mask(resolve_columns(columns)), op, int(streams)),
-                    "pkt_mgpu_parse_steps")
+        mask = ctypes.c_uint64(schema.column_mask(resolve_columns(columns)))
+        f, mg, cnt, ent, st = self._L.pkt_mgpu_parse_steps, self._mg, ctypes.c_int(count), ctypes.c_int(e), ctypes.c_int(streams)
+
+        def call():
+            rc = f(mg, bp, cnt, ent, mask, op, st)
+            if rc != 0:
+                self._check(rc, "pkt_mgpu_parse_steps")
+        call.keep = (plan, bp, op)  # the arrays the pointers point into
+        return call
+
+    def parse_steps(self, plan, entry="parse", columns="all", first=0, count=None, streams=2):
+        """steps_call(...)() — build and issue in one go."""
+        self.steps_call(plan, entry, columns, first, count, streams)()
 
     # ---------------------------------------------------------------- parse + gather
     def alloc_shard_outputs(self, shards, columns):

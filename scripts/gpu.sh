@@ -11,7 +11,7 @@
 #   bench[=ARGS]       python bench.py ARGS (default: the driver's --steps 20 --warmup 5)
 #   prof[=CFG]         rocprofv3 --kernel-trace --stats of bench.py --config CFG (one stream)
 #   traffic[=CFG]      FETCH_SIZE (x2, gfx950) and WRITE_SIZE passes of the same -> traffic.json
-#   kbench=CFG:VARS:WINDOWS   scripts/kbench.py, 1 and 2 streams, 3 rounds
+#   kbench=CFG:VARS:WINDOWS:STAGING   scripts/kbench.py, 1 and 2 streams, 3 rounds
 #   anat=CFG           memory-side request anatomy by column set (scripts/gpu_c4anat.sh)
 #   sq=CFG:VARS        SQ / LDS / TCC counter passes of kbench (scripts/pmc.sh + pmc_summary.py)
 #   stamps             per-wave segment stamps (needs lib/variants/stamps.so: build_variant.sh stamps -DPKTGPU_STAMPS=1)
@@ -49,15 +49,15 @@ for step in "$@"; do
            run write_$c 300 rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write_$c" -o pmc -- \
                python bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline --no-c5 --no-extra --streams 1
            run traffic_$c 60 python scripts/traffic.py "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c" "$OUT/traffic_$c.json" parse_kernel "$TAG $c" ;;
-    kbench) IFS=: read -r c v w <<< "$arg"
-           run kbench_$c 300 python scripts/kbench.py --config $c --variants "${v:-status;chain;all}" --windows ${w:-0} \
-               --streams 1,2 --rounds 3 --iters 24 ;;
+    kbench) IFS=: read -r c v w st <<< "$arg"
+           run kbench_${c}_st${st:-0} 300 python scripts/kbench.py --config $c --variants "${v:-status;chain;all}" --windows ${w:-0} \
+               --staging ${st:-0} --streams 1,2 --rounds 3 --iters 24 ;;
     anat)  run anat_${arg:-c4} 900 bash scripts/gpu_c4anat.sh ${TAG}_anat ;;
     sq)    IFS=: read -r c v <<< "$arg"
            run sq_$c 600 bash scripts/pmc.sh ${TAG}_sq_$c "${v:-all}" $c
            python scripts/pmc_summary.py gpurun_out/${TAG}_sq_$c > "$OUT/sq_$c.txt"; cat "$OUT/sq_$c.txt" ;;
     stamps) run stamps 600 bash -c 'export PKTGPU_LIB=packet-rs_amd/lib/variants/stamps.so;
-               for s in "c4 all 0" "c4 all 64" "c2 chain,ether,ipv4,udp 0" "c3 chain,ether,vlan,ipv4,tcp,udp 0"; do
+               for s in "c4 all 64" "c4 all 128"; do
                  set -- $s; python scripts/stamps.py --config $1 --columns $2 --window $3 || exit $?; done
                python scripts/stamps_pcap.py' ;;
     pcapab) run pcapab 900 bash -c 'for rep in 1 2 3; do for v in packet-rs_amd/lib/variants/p*.so; do

@@ -21,11 +21,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--config", default="c4")
 ap.add_argument("--columns", default="all")
 ap.add_argument("--window", type=int, default=0)
+ap.add_argument("--staging", type=int, default=0)
 ap.add_argument("--n", type=int, default=1 << 20)
 a = ap.parse_args()
 assert "stamps" in os.environ.get("PKTGPU_LIB", ""), "run with PKTGPU_LIB=.../variants/stamps.so"
 P = pktgpu.Parser(0)
 P.set_window(a.window)
+P.set_staging(a.staging)
 n = a.n
 if a.config == "c2":
     slab_np, stride, offs, lens = gen.gen_c2(n).reshape(-1), 64, None, None
