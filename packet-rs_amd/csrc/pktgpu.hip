@@ -568,17 +568,25 @@ __device__ __forceinline__ void tile_stage(uint8_t* lds, uint32_t wl, uint32_t w
     }
 }
 
-// resident waves per SIMD the pipelined kernel is compiled for (VGPRs hold the next tile's chunks)
-__host__ __device__ constexpr int pipe_waves_per_eu(int nch) { return nch >= 9 ? 4 : 6; }
+// Resident waves per SIMD the pipelined kernel is compiled for (VGPRs hold the next tile's chunks):
+// the most that compile without VGPR spills.  (A spilling build gave the last, partly active tile
+// of a batch wrong chains on some runs — spill slots written under a partial exec mask and read
+// back by the cross-lane chunk assignment — so every instantiation must stay spill-free:
+// `make asm`, build/resource-usage.txt.)
+__host__ __device__ constexpr int pipe_waves_per_eu(int nch, uint32_t gm) {
+    const bool fields = (gm & ~(uint32_t)(G_CHAIN | G_NT)) != 0;
+    return nch >= 9 ? (fields ? 3 : 4) : nch >= 5 ? (fields ? 4 : 5) : (fields ? 5 : 6);
+}
 template <int NCH, uint32_t GM, int WK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu(NCH))))
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu(NCH, GM))))
 void parse_pipe_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
     const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
     const uint32_t ntiles = (p.n + 63u) / 64u;
     const uint32_t W = gridDim.x * (uint32_t)kWavesPerBlock;
-    uint32_t tile = blockIdx.x * (uint32_t)kWavesPerBlock + (threadIdx.x >> 6);  // wave-uniform
+    // wave-uniform (an SGPR: the loop and its branches stay scalar, no exec-mask bookkeeping)
+    uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)kWavesPerBlock + (threadIdx.x >> 6));
     uint64_t off, off1, off2;
     uint32_t len, len1, len2;
     u32x4 ch[NCH];
@@ -622,7 +630,7 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const uint32_t per_cu = std::max<uint32_t>(
             1u, std::min<uint32_t>((uint32_t)((160u * 1024u) / window_lds(NCH)),
-                                   (uint32_t)(4 * pipe_waves_per_eu(NCH) / kWavesPerBlock)));
+                                   (uint32_t)(4 * pipe_waves_per_eu(NCH, GM) / kWavesPerBlock)));
         const uint32_t tiles = (kp.n + 63u) / 64u;
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus * per_cu, (tiles + kWavesPerBlock - 1) / kWavesPerBlock));
         hipLaunchKernelGGL((parse_pipe_kernel<NCH, GM, WK>), dim3(blocks), dim3(kBlock), window_lds(NCH), s, kp);
