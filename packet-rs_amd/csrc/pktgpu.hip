@@ -49,6 +49,22 @@ __device__ __forceinline__ void st(T* base, uint32_t boff, T v) {
         *reinterpret_cast<T*>(reinterpret_cast<char*>(base) + boff) = v;
 }
 
+// Record (type, offset) in header slot `slot` of packet i (slot-major columns, row stride ns = the
+// batch size): 32-bit byte offsets from the column bases while every slot row of the batch lies
+// within 4 GiB of them (ns <= 2^27, a wave-uniform branch), the 64-bit products beyond.
+template <uint32_t GM>
+__device__ __forceinline__ void push_slot(const pkt_out_t& out, uint64_t ns, uint32_t slot, uint32_t i, uint32_t ty,
+                                          uint32_t o) {
+    if (ns <= (1ull << 27)) {
+        const uint32_t e = slot * (uint32_t)ns + i;
+        if (want<GM, G_CHAIN>(out.hdr_type)) st<false, uint8_t>(out.hdr_type, e, (uint8_t)ty);
+        if (want<GM, G_CHAIN>(out.hdr_off)) st<false, uint16_t>(out.hdr_off, 2u * e, (uint16_t)o);
+    } else {
+        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)ty;
+        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
+    }
+}
+
 // Fields of the first header of each group (Q11), from the walk's first offsets.
 // `i` is the packet index within this launch (< kLaunchChunk = 2^26, so every per-packet byte
 // offset, up to i * 16 for the IPv6 addresses, fits 32 bits).
@@ -272,9 +288,10 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
 // over the tiles, each lane's loads of its next packet in flight while it parsed the current one,
 // was measured no faster at k = 4 and slower at k = 1, 2: DESIGN.md §5.)
 // Resident waves per SIMD the compiler may assume (VGPR budget 512 / waves): 8 for fixed-stride
-// windows (<= 64 VGPRs); 4 for the 144-byte indexed windows, whose 37.9 KB of LDS per block allows 4
-// blocks per CU anyway; wider windows unconstrained.
-__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch == 9 ? 4 : 8); }
+// windows (<= 64 VGPRs); for indexed windows what their LDS allows anyway — 6 for the 96-byte
+// windows (25.6 KB per block, 6 blocks per CU), 4 for the 144-byte ones (37.9 KB, 4 blocks); wider
+// windows unconstrained.
+__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : 6) : 8); }
 template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
 void parse_kernel(KParams p) {
@@ -376,10 +393,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     // isolated launches, slower pipelined steps)
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
-    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
-        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i_own] = (uint8_t)ty;
-        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i_own] = (uint16_t)o;
-    };
+    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) { push_slot<GM>(out, ns, slot, i_own, ty, o); };
     // fast.rs:5-12 (>= 1500) -> parse_ethernet 35-48 (0x8100 -> parse_vlan 49-62, repeated;
     // 0x0800) -> parse_ipv4 84-98 (17 / 6) -> parse_udp 208-217 (dst != 4789) | parse_tcp 203-207
     // -> accept 223-227
@@ -511,10 +525,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     }
     const pkt_out_t& out = p.out;
     const uint64_t ns = p.n_slot_stride;
-    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) {
-        if (want<GM, G_CHAIN>(out.hdr_type)) out.hdr_type[(uint64_t)slot * ns + i] = (uint8_t)ty;
-        if (want<GM, G_CHAIN>(out.hdr_off)) out.hdr_off[(uint64_t)slot * ns + i] = (uint16_t)o;
-    };
+    auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) { push_slot<GM>(out, ns, slot, i, ty, o); };
     WalkResult r;
     walk<WK>(pv, entry_state(p.entry), active, push, r);
     if (!active) return;
@@ -575,7 +586,7 @@ __device__ __forceinline__ void tile_stage(uint8_t* lds, uint32_t wl, uint32_t w
 // `make asm`, build/resource-usage.txt.)
 __host__ __device__ constexpr int pipe_waves_per_eu(int nch, uint32_t gm) {
     const bool fields = (gm & ~(uint32_t)(G_CHAIN | G_NT)) != 0;
-    return nch >= 9 ? (fields ? 3 : 4) : nch >= 5 ? (fields ? 4 : 5) : (fields ? 5 : 6);
+    return nch >= 9 ? (fields ? 3 : 4) : nch >= 6 ? 4 : nch >= 5 ? (fields ? 4 : 5) : (fields ? 5 : 6);
 }
 template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu(NCH, GM))))
@@ -622,7 +633,7 @@ enum LaunchMode { M_TILE = 0, M_SPAN = 2, M_PIPE = 3 };
 
 template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
-    if constexpr (NCH == 4 || NCH == 5 || NCH == 9) if (mode == M_PIPE) {
+    if constexpr (NCH == 4 || NCH == 6 || NCH == 9) if (mode == M_PIPE) {
         // persistent: as many blocks as reside on a CU (its LDS over the block's windows, and the
         // waves per SIMD the kernel is compiled for), at most one wave per tile
         int cus = 256, dev = 0;
@@ -651,7 +662,9 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
 hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s) {
-    if (wk == 1) {  // indexed batches: non-temporal column stores
+    // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 9 and
+    // 17 chunks only (parse_impl widens a narrower request)
+    if constexpr (NCH >= 6) if (wk == 1) {
         switch (gm) {
             case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s);
             case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s);
@@ -901,13 +914,13 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Window: bytes of each packet staged in LDS.  Fixed stride: the slot (up to 128 B);
     // indexed: 128 B.  Unaligned packet starts need one more chunk.
     uint32_t w = ctx->window;
-    // Auto window: 64 bytes of the packet (80 from its 16-byte-aligned start for indexed
-    // batches), which hold every header of the common chains (Ether[/Vlan x2]/IPv4/TCP ends at
-    // byte 62); deeper chains (tunnels) read the rest through L2.  A 128-byte window
-    // (pkt_ctx_set_window(ctx, 128): every header of the 22 reference templates in LDS, C4 line
-    // requests 2.28M -> 1.61M per 2^20 records) measured slower: 37.9 KB of LDS per block allows
-    // 4 blocks per CU instead of 7 (C4 pipelined 81 vs 76 us, isolated equal).
-    if (w == 0) w = b->offsets ? 64u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
+    // Auto window: the stride up to 64 bytes for fixed-stride slabs (Ether[/Vlan x2]/IPv4/TCP ends at
+    // byte 62); 80 bytes for indexed batches (96 from the record's 16-byte-aligned start: every
+    // header of 16 of the 22 reference templates, the rest read past it through L2).  C4 per 2^20
+    // records, same box, 2 streams: 80 B 46.6 (chain) / 68.1 us (all columns), 64 B 49.4 / 75.8,
+    // 96 B 49.6 / 69.1, 128 B 59.7 / 77.4 — wider windows read fewer lines twice but hold fewer
+    // waves per CU (LDS), round 3.
+    if (w == 0) w = b->offsets ? 80u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);
@@ -922,6 +935,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
+    if (wk == 1 && nch < 6) nch = 6;  // the narrowest lockstep build
     for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kLaunchChunk) {
         const uint64_t cnt = std::min<uint64_t>(kLaunchChunk, b->n - i0);
         KParams kp;
@@ -945,6 +959,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         if (nch <= 2) e = launch_gm<2>(kp, gm, mode, wk, s);
         else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, wk, s);
         else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, wk, s);
+        else if (nch <= 6) e = launch_gm<6>(kp, gm, mode, wk, s);
         else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, wk, s);
         else e = launch_gm<17>(kp, gm, mode, wk, s);
     }

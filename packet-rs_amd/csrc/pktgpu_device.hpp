@@ -437,11 +437,16 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
             q += 8;
         }
     }
-    // commit (lanes not taking part keep their state)
-    L.steps = live ? steps : L.steps;
-    L.pay = (live && acc && f == 0) ? o : L.pay;
-    L.status = (live && f) ? f : L.status;
-    L.live = go && f == 0;
+    // commit (lanes not taking part keep their state).  A lane whose next state is ACCEPT takes
+    // that step now instead of in one more iteration (fast.rs:223-227: the payload starts at q),
+    // with the walk's iteration bound for it — the only check the accept step has.
+    const bool cont = go && f == 0;
+    const bool facc = cont && nx == S_ACCEPT;
+    const uint32_t fa = (steps + 1 > PKT_MAX_HDRS + 3) ? (uint32_t)PKT_DEPTH_LIMIT : 0u;
+    L.steps = live ? steps + (facc ? 1u : 0u) : L.steps;
+    L.pay = (live && acc && f == 0) ? o : ((facc && fa == 0) ? q : L.pay);
+    L.status = (live && f) ? f : ((facc && fa) ? fa : L.status);
+    L.live = cont && !facc;
     L.o = live ? q : L.o;
     L.st = live ? nx : L.st;
 }
@@ -460,6 +465,16 @@ __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active
                                      WalkResult& out) {
     if constexpr (WK == 1) {
         LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active, {-1, -1, -1, -1, -1, -1}};
+        if (state == S_PARSE) {
+            // fast.rs:5-12's dispatch, lstep's PARSE case taken before the loop (no record, no
+            // offset change): >= 14 bytes go to Dot3 (EtherType field < 1500) or Ether, shorter
+            // records are truncated
+            const uint32_t hw = active ? pv.be16(12) : 0u;
+            L.steps = active ? 1u : 0u;
+            L.status = (active && pv.len < 14u) ? (uint32_t)PKT_TRUNCATED : (uint32_t)PKT_OK;
+            L.live = active && pv.len >= 14u;
+            L.st = hw < 1500u ? S_DOT3 : S_ETHER;
+        }
         const uint32_t* w = reinterpret_cast<const uint32_t*>(pv.lw);
         while (__ballot(L.live)) {
             const bool live = L.live;

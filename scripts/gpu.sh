@@ -15,7 +15,7 @@
 #   anat=CFG           memory-side request anatomy by column set (scripts/gpu_c4anat.sh)
 #   sq=CFG:VARS        SQ / LDS / TCC counter passes of kbench (scripts/pmc.sh + pmc_summary.py)
 #   stamps             per-wave segment stamps (needs lib/variants/stamps.so: build_variant.sh stamps -DPKTGPU_STAMPS=1)
-#   pcapab             pcap indexer variants lib/variants/p*.so, interleaved (scripts/pcap_index_bench.py)
+#   pcapab             pcap indexer variants lib/variants/*.so, interleaved (scripts/pcap_index_bench.py)
 #   pcap               pcap indexer rate + rocprofv3 kernel stats of it
 #   secondary          §8(f) kernels: scripts/secondary_bench.py + rocprofv3 kernel stats
 #   host               host-memory path rates (scripts/hostpath_native.py, pinned and pageable)
@@ -53,14 +53,14 @@ for step in "$@"; do
            run kbench_${c}_st${st:-0} 300 python scripts/kbench.py --config $c --variants "${v:-status;chain;all}" --windows ${w:-0} \
                --staging ${st:-0} --streams 1,2 --rounds 3 --iters 24 ;;
     anat)  run anat_${arg:-c4} 900 bash scripts/gpu_c4anat.sh ${TAG}_anat ;;
-    sq)    IFS=: read -r c v <<< "$arg"
-           run sq_$c 600 bash scripts/pmc.sh ${TAG}_sq_$c "${v:-all}" $c
-           python scripts/pmc_summary.py gpurun_out/${TAG}_sq_$c > "$OUT/sq_$c.txt"; cat "$OUT/sq_$c.txt" ;;
+    sq)    IFS=: read -r c v <<< "$arg"; n=sq_${c}_$(echo "${v:-all}" | tr -c 'a-z0-9' '_')
+           run $n 600 bash scripts/pmc.sh ${TAG}_$n "${v:-all}" $c
+           python scripts/pmc_summary.py gpurun_out/${TAG}_$n > "$OUT/$n.txt"; cat "$OUT/$n.txt" ;;
     stamps) run stamps 600 bash -c 'export PKTGPU_LIB=packet-rs_amd/lib/variants/stamps.so;
                for s in "c4 all 64" "c4 all 128"; do
                  set -- $s; python scripts/stamps.py --config $1 --columns $2 --window $3 || exit $?; done
                python scripts/stamps_pcap.py' ;;
-    pcapab) run pcapab 900 bash -c 'for rep in 1 2 3; do for v in packet-rs_amd/lib/variants/p*.so; do
+    pcapab) run pcapab 900 bash -c 'for rep in 1 2 3; do for v in packet-rs_amd/lib/variants/*.so; do
                PKTGPU_LIB=$v python scripts/pcap_index_bench.py --reps 20 | sed "s|^|$(basename $v) |" || exit $?; done; done' ;;
     pcap)  run pcap 300 python scripts/pcap_index_bench.py --reps 20
            run pcap_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pcap_prof" -o trace -- \
@@ -70,7 +70,7 @@ for step in "$@"; do
                python scripts/secondary_bench.py --cpu-budget 0.2 ;;
     host)  run host 600 bash -c 'for c in c2 c4; do python scripts/hostpath_native.py --config $c --chunks 262144 || exit $?;
                python scripts/hostpath_native.py --config $c --pageable --chunks 131072,262144 || exit $?; done' ;;
-    ab)    IFS=: read -r c v <<< "$arg"; run ab 900 bash scripts/ab.sh "${c:-c2}" "${v:-status;chain;all}" 2 ;;
+    ab)    IFS=: read -r c v <<< "$arg"; run ab_${c:-c2} 900 bash scripts/ab.sh "${c:-c2}" "${v:-status;chain;all}" 2 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
