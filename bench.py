@@ -233,6 +233,9 @@ def load_probe():
     L.pkt_probe_ceiling.restype = ctypes.c_int
     L.pkt_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.POINTER(_lib.PktOut), ctypes.c_void_p]
+    L.pkt_probe_ceiling_groups.restype = ctypes.c_int
+    L.pkt_probe_ceiling_groups.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.POINTER(_lib.PktOut), ctypes.c_void_p]
     return L
 
 
@@ -342,21 +345,27 @@ WORKLOAD = {"c2": "C2: 2^20 x 64 B Ether/IPv4/UDP fixed-stride slab per GPU",
             "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}
 
 
-def roofline_phase(args, torch, P, batches, ostructs, raw_slabs, ring, n, stride, entry, default_cols, dev):
+def roofline_phase(args, torch, P, batches, ostructs, raw_slabs, ring, n, stride, entry, default_cols, dev,
+                   slots):
     """The parse kernel in isolation on device 0 — R back-to-back launches on ONE stream between one
     event pair on that stream — alternated with the ceiling probe (same launch shape, same bytes, no
-    parsing; C2-shaped configs only) and a device copy of the slab.  Median of 5 rounds each."""
+    parsing; the fixed-stride configs C2 and C3 with their default columns, `slots` header slot rows)
+    and a device copy of the slab.  Median of 5 rounds each."""
     import ctypes
     R = min(max(args.steps, 20), 50)
     rs = torch.cuda.Stream(dev)
-    probe = load_probe() if (args.config in ("c2", "c5") and args.columns == default_cols) else None
+    probe = load_probe() if (args.config in ("c2", "c3", "c5") and args.columns == default_cols) else None
 
     def parse_launch(k, s):
         P.launch(batches[k % ring], entry, ostructs[k % ring], s)
 
     def probe_launch(k, s):
-        rc = probe.pkt_probe_ceiling(ctypes.c_void_p(raw_slabs[k % ring].data_ptr()), n, stride,
-                                     ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
+        if args.config == "c3":
+            rc = probe.pkt_probe_ceiling_groups(ctypes.c_void_p(raw_slabs[k % ring].data_ptr()), n, stride, slots,
+                                                ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
+        else:
+            rc = probe.pkt_probe_ceiling(ctypes.c_void_p(raw_slabs[k % ring].data_ptr()), n, stride,
+                                         ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
         if rc != 0:
             raise RuntimeError(f"pkt_probe_ceiling failed ({rc})")
 
@@ -404,7 +413,7 @@ def assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, s
     if ceil_:
         cs = float(np.median(ceil_)) * 1e-3
         res["roofline"]["ceiling"] = {
-            "kernel": "pkt_probe_ceiling (libpktprobe.so): same launch shape and bytes, no parsing",
+            "kernel": "pkt_probe_ceiling (C2) / pkt_probe_ceiling_groups (C3), libpktprobe.so: same launch shape and bytes, no parsing",
             "avg_kernel_us": round(cs * 1e6, 3), "achieved": round(algo / cs / 1e9, 2),
             "frac_of_peak": round(algo / cs / 1e9 / HBM_PEAK_GBS, 4),
             "parse_frac_of_ceiling": round(cs / avg_kern_s, 4)}
@@ -567,15 +576,15 @@ def run_mgpu(args, ndev):
     p0 = per[0]
     batches0 = [P._batch(p0["slabs"][r], n, p0["stride"], p0["offs"], p0["lens"]) for r in range(ring)]
     ostructs0 = [P.out_struct(p0["outs"][r][1]) for r in range(ring)]
+    o0 = p0["outs"][0][1]
+    used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
     R, kern, ceil_, copy_ = roofline_phase(args, torch, P, batches0, ostructs0, p0["slabs"], ring, n, p0["stride"],
-                                           entry, default_cols, MP.torch_devices[0])
+                                           entry, default_cols, MP.torch_devices[0], used_slots)
 
     c5 = None
     if args.config == "c2" and not args.no_c5:
         c5 = run_c5_mgpu(args, torch, MP, per, cols, entry)
 
-    o0 = p0["outs"][0][1]
-    used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
     span = o0["payload_off"].cpu().numpy() if "payload_off" in o0 else np.full(n, 64, np.int64)
     read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
     algo = read_b + write_b

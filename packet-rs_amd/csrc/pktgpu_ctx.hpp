@@ -23,10 +23,12 @@ struct HostPipe {
 
 // Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.
 struct PcapScratch {
-    void* buf = nullptr;   // regions x (entry u64, exit u64, count u32, err u32) + record lists + scan
+    void* buf = nullptr;   // the tile ticket + one published state per 16 KiB tile
     uint64_t bytes = 0;
-    uint64_t* ctl = nullptr;      // pinned host words the indexer reads back (change count, totals)
-    uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the scan kernel writes them)
+    uint64_t* ctl = nullptr;      // pinned host words the indexer reads back (magic, total, error)
+    uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the kernel writes them)
+    uint32_t epoch = 0;           // per call: block states of older calls are ignored, not cleared
+    uint32_t scan_resident = 0;   // scan-kernel blocks resident at once (0 = not yet queried)
 };
 
 // Element size of each pkt_out_t column, in declaration order (slot columns: one slot; the

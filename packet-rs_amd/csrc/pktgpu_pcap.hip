@@ -8,30 +8,31 @@
 // behaviour are pkt_pcap_index's (pktgpu_host.cpp): records are taken while 16 header bytes
 // remain; a record running past the end is an error; a shorter tail is ignored.
 //
-// The record chain is sequential (each header says where the next one starts), so the file is cut
-// into 4 KiB regions, one wave each, and the chain is recovered by speculation plus a fix-up:
-//   GUESS   a block stages 4 consecutive regions (16 KiB + 16 B) in LDS; each wave finds the
-//           first offset of its region from which a chain of plausible record headers runs (64
-//           offsets per step, one per lane; hops past the staged block read global memory), walks
-//           the records from there and keeps (entry, exit, count, error) and the records' offsets
-//           in the region (u16 list).  Region 0's entry is 24, by definition.
-//   REPAIR  one thread per region compares its entry with the exit of the nearest non-empty
-//           region to its left.  A region that disagrees while that neighbour agrees with its own
-//           left is queued; the block's waves re-walk each queued region from that exit and chase
-//           on into the following regions until an exit meets the next region's stored entry.
-//           Every region left of the first disagreement is exact (region 0 is, and each agrees
-//           with an exact left), so the first queued chase is exact and no round ends without
-//           fixing at least that region; a round in which no region disagrees is the exact fixed
-//           point — the true chain, whatever the guesses were.  A chase claims each region before
-//           rewriting it (atomicMax of the round id on the region's owner word) and stops at a
-//           region another chase already claimed this round, so a region's entry, exit, count,
-//           error and list always come from ONE walk; the first queued chase cannot be stopped
-//           (chases only move right and start at queued regions), which keeps the progress bound.
-//   SCAN    exclusive prefix of the per-region counts (per 1024 regions; the last block to finish
-//           scans the block totals).
-//   EMIT    256 threads write 16 regions' records at their prefix: offset = pos + 16, incl_len =
-//           next pos - pos - 16 (the last one from the region's exit); the file is not re-read.
-// HBM traffic ≈ the file once + 2 B/record (the list) written and read + 12 B/record of output.
+// The record chain is sequential (each header says where the next one starts): speculation per
+// 4 KiB region, then an exact pass over the regions' states, then the output.  Three kernels, one
+// host read-back:
+//   GUESS (pcap_guess_kernel)  a block stages 4 consecutive regions (16 KiB) in LDS; each wave
+//            finds the first offset of its region from which a chain of plausible record headers
+//            runs (64 candidates per step, one per lane) — or "none" — and walks the records from
+//            it: per region entry, exit, count (+ error bit) and the records' u16 offsets.  Region
+//            0's entry is 24 by definition.  No block waits for another.
+//   SCAN (pcap_scan_kernel)  a block takes the next 256 regions (a ticket, so every lower block
+//            is already running) and composes their states (combine() below: associative, and it
+//            carries consistency — a region's state is exact iff its entry equals the exact exit of
+//            the region before, "none" iff that exit lies past it, so a composition from offset 24
+//            that is consistent at every seam IS exact).  Wrong guesses (a plausible-looking chain
+//            inside a payload) show up as inconsistent seams: a region that disagrees with the
+//            claiming region before it, while that one agrees with its own left, is re-walked from
+//            its exit (stage the 4 KiB, walk: a few us, rare).  The block publishes its aggregate,
+//            composes the published states of the blocks before it (256 per round trip, stopping at
+//            the nearest exact one), fixes its own first seam against that exact exit if needed,
+//            publishes its exact state, and writes each region's exact record prefix.  The last
+//            block writes the total and the error flag to pinned host words.
+//   EMIT (pcap_emit_kernel)  16 regions per block, one record per thread: offset = pos + 16,
+//            incl_len = next pos - pos - 16 (the last one from the region's exit).
+// tests/test_pcap_model.py restates the composition and the fixes and checks them against the host
+// indexer on captures built to defeat the guess.  HBM traffic ≈ the file once + 2 B/record of
+// record lists written and read + 12 B/record of output.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -41,46 +42,60 @@
 
 namespace {
 
-#ifndef PKTGPU_PCAP_REGION
-#define PKTGPU_PCAP_REGION 4096
-#endif
-constexpr uint32_t kRegion = PKTGPU_PCAP_REGION;  // bytes of record starts per region
+constexpr uint32_t kRegion = 4096;                // bytes of record starts per region
 static_assert(kRegion % 16 == 0 && kRegion / 16 <= 65536, "u16 record lists");
 constexpr uint32_t kMaxRec = kRegion / 16;       // records per region (each >= 16 B apart)
-constexpr int kWaves = 4;                         // waves per 256-thread block
-constexpr uint32_t kBlockBytes = kWaves * kRegion;
-constexpr uint32_t kScanBlock = 1024;             // regions per first-level scan block
-constexpr uint32_t kEmitRegions = 16;             // regions per emit block
-constexpr int kLookback = 64;                     // empty regions skipped when finding an entry
-constexpr int kChaseMax = 256;                    // regions one repair chase may rewrite
-#ifndef PKTGPU_PCAP_HOPS
-#define PKTGPU_PCAP_HOPS 2, 2  // (min, max); 3, 4: 117 us per call, 2, 3: 112, 2, 2: 108 (profiles/ab/r02hops_*)
-#endif
-constexpr int kHops[2] = {PKTGPU_PCAP_HOPS};
-constexpr int kMinHops = kHops[0], kMaxHops = kHops[1];  // guess chain length
+constexpr int kWaves = 4;                         // waves (regions) per 256-thread block
+constexpr int kMinHops = 2, kMaxHops = 2;         // guess chain length (3-4 hops measured slower)
 constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec within a day
-constexpr uint32_t kPassSlots = 64;               // passes with their own control words
-// Repair rounds per pass: 2.  With 1, the C4 capture's first pass always still finds a guess to fix
-// and needs a second pass (one more read-back): 141 vs 111 us per call (round 3, same box).
-constexpr uint32_t kRounds = 2;
 
-// Control words (device, zeroed once per call): [0] magic is d4 c3 b2 a1; then per pass p (slot
-// p % 64): [8 + 8s + 2r] regions that disagreed in round r, [9 + 8s + 2r] K - first such region
-// (max; 0 = none), [12 + 8s] a region's walk hit a record running past the end, [13 + 8s] the
-// record total, [14 + 8s] the scan's block ticket.
-constexpr uint32_t kCtlWords = 8 + 8 * kPassSlots;
+// Host-visible words (pinned, written by the kernels).
+enum : int { kHostMagic = 0, kHostTotal = 1, kHostErr = 2, kHostWords = 4 };
+
+// A scan block's published states: its aggregate (a_*) once its own seams are consistent, its
+// exact inclusive state (i_*) once it knows the exact exit before it.  meta = epoch << 8 | bits
+// (| 16 = published): states of older calls carry older epochs, so the array needs no per-call reset.
+struct alignas(64) BlkDesc {
+    uint64_t a_first, a_last, a_cnt, a_meta;
+    uint64_t i_last, i_cnt, i_meta, pad;
+};
+enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4, kPublished = 16 };
+
+constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
+constexpr uint32_t kEmitRegions = 16;   // regions per emit block
 
 struct Scratch {
-    uint64_t* entry;   // first record start >= region start (may lie past the region)
-    uint64_t* exit;    // first record start >= region end, as walked from entry
-    uint32_t* cnt;     // records starting in the region
-    uint32_t* err;     // the walk met a record running past the end of the file
-    uint32_t* pre;     // exclusive prefix of cnt within its scan block
-    uint64_t* bpre;    // exclusive prefix of the scan blocks
+    uint64_t* rentry;  // per region: the walk's entry (>= the region's end: no record starts in it)
+    uint64_t* rexit;   // per region: exit (first record start >= the region's end, as walked)
+    uint32_t* rcnt;    // per region: records, bit 31 = the walk met a record running past the end
+    uint64_t* rpre;    // per region: records before it in the file (exact; the scan writes it)
     uint16_t* list;    // [region][kMaxRec] record offsets relative to the region base
-    uint32_t* own;     // the last repair round whose chase rewrote the region (0 = none)
-    uint64_t* ctl;     // control words above
+    BlkDesc* blk;      // one per scan block
+    uint32_t* ticket;  // the scan kernel's
+    uint64_t* host;    // kHostWords pinned words (device address)
+    uint32_t epoch;
 };
+
+// The aggregate of a run of regions:
+//   none (kBitNone): no region of the run claims a record start; consistent with a predecessor
+//     exit e iff e >= last (the run's end), which it passes through;
+//   otherwise: `first` = the entry of its first claiming region, `last` = the exit of its last,
+//     `cnt` records, kBitBad if two of its regions disagree, kBitErr if a walk met a record
+//     running past the end of the file.  Consistent with e iff e == first and not bad.
+// combine(a, b) for a run a followed by run b is associative; none(0) is its identity.
+struct Agg {
+    uint64_t first, last, cnt;
+    uint32_t bits;
+};
+__device__ __forceinline__ Agg agg_identity() { return Agg{0, 0, 0, kBitNone}; }
+__device__ __forceinline__ Agg combine(const Agg& a, const Agg& b) {
+    if (a.bits & kBitNone) {
+        if (b.bits & kBitNone) return Agg{0, a.last > b.last ? a.last : b.last, 0, kBitNone};
+        return b;
+    }
+    if (b.bits & kBitNone) return Agg{a.first, a.last, a.cnt, a.bits | (a.last < b.last ? kBitBad : 0u)};
+    return Agg{a.first, b.last, a.cnt + b.cnt, a.bits | b.bits | (a.last != b.first ? kBitBad : 0u)};
+}
 
 __device__ __forceinline__ uint32_t lane_id() {
     return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -100,7 +115,7 @@ __device__ __forceinline__ uint32_t ld32(const uint32_t* lw, uint32_t o) {
 
 // A record header a real capture could hold: microseconds < 1e6, 0 < incl_len <= snaplen,
 // incl_len <= orig_len <= 1 MiB, and the record ends inside the file.  Only a heuristic for the
-// guess; the repair rounds make the result exact whatever it accepts.
+// guess; the look-back makes the result exact whatever it accepts.
 struct RecHdr {
     uint32_t sec, usec, incl, orig;
 };
@@ -172,16 +187,9 @@ __device__ __forceinline__ bool chain_global(const uint32_t* lw, const uint8_t* 
     return true;
 }
 
-// The nearest region left of k that claims a record start (entry inside it), or region 0.
-__device__ __forceinline__ uint32_t left_of(const Scratch& S, uint32_t k) {
-    uint32_t j = k - 1;
-    for (int s = 0; s < kLookback && j > 0 && S.entry[j] >= (uint64_t)(j + 1) * kRegion; s++) j--;
-    return j;
-}
-
-// Stage file bytes [base, base + BYTES + 16) into LDS, zeros past the file's 16-byte-rounded end,
-// plus 16 zero bytes of pad; NT threads, this one is `t`.  All loads are issued before the first
-// LDS write (one memory latency per stage, not one per piece).
+// Stage file bytes [base, base + BYTES + 16) into LDS, zeros past the file's 16-byte-rounded end;
+// NT threads, this one is `t`.  All loads are issued before the first LDS write (one memory
+// latency per stage, not one per piece).
 template <uint32_t BYTES, uint32_t NT>
 __device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t base, uint64_t len, uint32_t t) {
     constexpr uint32_t kPieces = BYTES / 16 + 2, kPer = (kPieces + NT - 1) / NT;
@@ -203,13 +211,12 @@ __device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t ba
 // region is kept by lane i in `rec` (a select per record, no branch, no LDS write); records 64..
 // (regions of short records) go to `list` from lane 0.  The position lives in an SGPR
 // (readfirstlane of each LDS read), so the loop's bounds checks are SALU compares and its branches
-// uniform (round 3: guess kernel + 2 repair rounds + scan + emit 111-114 -> 101-102 us per
-// 2^20-record call; the round-1 SGPR walk kept 64-bit positions and measured slower), with 32-bit
-// offsets from lbase while the file's end is < 4 GiB past it; otherwise the 64-bit vector form.
+// uniform, with 32-bit offsets from lbase while the file's end is < 4 GiB past it; otherwise the
+// 64-bit vector form.
 __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_t* list, uint64_t base,
                                      uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err,
                                      uint32_t& rec) {
-    if (len - lbase <= 0xFFFFFFF0ull) {
+    if (len - lbase <= 0xFFFFFFF0ull && entry - lbase <= 0xFFFFFFF0ull) {
         const uint32_t lane = lane_id();
         const uint32_t rb = (uint32_t)(base - lbase), rend = rb + kRegion, rlen = (uint32_t)(len - lbase);
         uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(entry - lbase));
@@ -222,7 +229,7 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
                 break;
             }
             rv = lane == c ? p - rb : rv;
-            if (c >= 64u && lane == 0) list[c] = (uint16_t)(p - rb);
+            if (c >= 64u && c < kMaxRec && lane == 0) list[c] = (uint16_t)(p - rb);
             c++;
             p += 16 + incl;
         }
@@ -247,263 +254,399 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
         }
         const uint32_t ro = (uint32_t)(pos - base);
         rec = lane == cnt ? ro : rec;
-        if (__builtin_amdgcn_readfirstlane(cnt) >= 64u && lane == 0) list[cnt] = (uint16_t)ro;
+        if (__builtin_amdgcn_readfirstlane(cnt) >= 64u && cnt < kMaxRec && lane == 0) list[cnt] = (uint16_t)ro;
         cnt++;
         pos += 16 + (uint64_t)incl;
     }
     exit = pos;
 }
 
-// Write a walked region back: the record offsets (lane i's register for record i < 64, the LDS
-// list beyond) and the region's words.
-__device__ __forceinline__ void store_region(const Scratch& S, uint32_t k, const uint16_t* list, uint32_t rec,
-                                             uint64_t entry, uint64_t exit, uint32_t cnt, uint32_t err) {
+// Region k's guessed entry (the candidate scan of the staged tile at lbase); base + kRegion =
+// "no record starts here".
+template <uint32_t STAGED>
+__device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf, uint64_t len, const uint32_t* lw,
+                                                uint64_t lbase, uint32_t k) {
     const uint32_t lane = lane_id();
-    uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
-    if (lane < cnt) dst[lane] = (uint16_t)rec;
-    for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = list[i];
-    if (lane == 0) {
-        S.entry[k] = entry;
-        S.exit[k] = exit;
-        S.cnt[k] = cnt;
-        S.err[k] = err;
+    const uint64_t lend = lbase + STAGED;
+    const uint64_t base = (uint64_t)k * kRegion;
+    // snaplen (global header bytes 16..19) bounds a plausible incl_len
+    uint32_t snap = *reinterpret_cast<const uint32_t*>(buf + 16);
+    if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
+    const uint64_t stop = len < base + kRegion ? len : base + kRegion;
+    const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
+    for (uint64_t c0 = base; c0 < stop; c0 += 64) {
+        // The lowest candidate whose chain checks out inside the staged bytes wins; only when
+        // there is none do the candidates whose chains leave them read global memory.
+        const uint64_t c = c0 + lane;
+        const int r = c < stop && c + 16 <= len
+                          ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
+                          : 0;
+        uint64_t m = __ballot(r == 1);
+        if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
+        if (m) return c0 + (uint64_t)__builtin_ctzll(m);
     }
+    return base + kRegion;
 }
 
-// Diagnostic build only (-DPKTGPU_STAMPS=1): s_memtime stamps per guess wave — start, staged,
-// entry found, walked, stored — to a debug buffer no other code reads (pkt_debug_pcap_stamps).
-#ifndef PKTGPU_STAMPS
-#define PKTGPU_STAMPS 0
-#endif
-#if PKTGPU_STAMPS
-__device__ uint64_t* g_pcap_stamps;
-#define PCAP_STAMP(k)                                                                         \
-    do {                                                                                      \
-        __builtin_amdgcn_sched_barrier(0);                                                    \
-        uint64_t t_;                                                                          \
-        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");            \
-        __builtin_amdgcn_sched_barrier(0);                                                    \
-        pst[k] = t_;                                                                          \
-    } while (0)
-#else
-#define PCAP_STAMP(k) \
-    do {              \
-    } while (0)
-#endif
+// Tile states cross XCDs (each XCD has its own L2): every access is a device-scope relaxed atomic
+// (performed at the device's coherence point), and a publication is ordered by waiting for the data
+// stores to complete before the flag store — no release/acquire fences, which on gfx950 write back /
+// invalidate the whole L2 at device scope.  (A single-pass form that did the look-back per 16 KiB
+// tile with a ticket per tile measured 160-436 us per 2^20-record call: 11.9K device-scope atomics
+// on one word serialise, and exact states can only advance 64 tiles per round trip.)
+template <class T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <class T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
-// One region's guess (wave w of the block whose 4 regions are staged at lbase): its entry by the
-// candidate scan, then its walk, stored to the region's words and list.
-__device__ __forceinline__ void guess_region(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K, const Scratch& S,
-                                             const uint32_t* lw, uint16_t* list, uint64_t lbase, uint32_t k,
-                                             uint64_t* pst) {
-    (void)pst;
-    const uint32_t lane = lane_id();
-    const uint64_t lend = lbase + kBlockBytes;
-    if (lane == 0) S.own[k] = 0;
+// Region k's aggregate from its (entry, exit, count|err) state; identity past the file.
+__device__ __forceinline__ Agg region_agg(uint32_t k, uint32_t K, uint64_t entry, uint64_t exit, uint32_t cw) {
+    if (k >= K) return agg_identity();
+    const uint64_t end = ((uint64_t)k + 1) * kRegion;
+    if (k != 0 && entry >= end) return Agg{0, end, 0, kBitNone};
+    return Agg{entry, exit, cw & 0x7FFFFFFFu, (cw >> 31) ? kBitErr : 0u};
+}
+
+// GUESS (file header): one region per wave, a block stages 4 consecutive regions (16 KiB + 16 B).
+// (One wave per 8 KiB tile walking its second region on from the first's exit — half the candidate
+// scans — measured slower: 77 vs 63 us per 2^20-record call; the kernel is bound by each wave's
+// chain of dependent LDS reads, and the 32-waves-per-CU cap is reached either way.)
+__global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
+                                                         Scratch S) {
+    constexpr uint32_t kStaged = kWaves * kRegion;
+    __shared__ uint4 lds[kStaged / 16 + 2];
+    __shared__ uint16_t lst[kWaves][kMaxRec];
+    const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
+    const uint64_t lbase = (uint64_t)blockIdx.x * kStaged;
+    stage<kStaged, 256>(lds, buf, lbase, len, t);
+    __syncthreads();
+    const uint32_t k = blockIdx.x * kWaves + w;
+    if (k >= K) return;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     const uint64_t base = (uint64_t)k * kRegion;
-    uint64_t entry = 24;
-    if (k == 0) {
-        if (lane == 0) S.ctl[0] = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
-    } else {
-        // snaplen (global header bytes 16..19) bounds a plausible incl_len
-        uint32_t snap = *reinterpret_cast<const uint32_t*>(buf + 16);
-        if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
-        const uint64_t stop = len < base + kRegion ? len : base + kRegion;
-        const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
-        entry = base + kRegion;  // none found: guess "no record starts here"
-        for (uint64_t c0 = base; c0 < stop; c0 += 64) {
-            // The lowest candidate whose chain checks out inside the staged bytes wins; only when
-            // there is none do the candidates whose chains leave them read global memory.
-            const uint64_t c = c0 + lane;
-            const int r = c < stop && c + 16 <= len
-                              ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), kBlockBytes, lim, snap)
-                              : 0;
-            uint64_t m = __ballot(r == 1);
-            if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
-            if (m) {
-                entry = c0 + (uint64_t)__builtin_ctzll(m);
-                break;
-            }
-        }
-    }
-    PCAP_STAMP(2);
+    const uint64_t entry = k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k);
     uint64_t exit;
     uint32_t cnt, err, rec;
-    walk(lw, lbase, list, base, entry, len, exit, cnt, err, rec);
+    // (the walk reading each incl_len by scalar-unit loads from L2 instead of LDS halves the VALU
+    // instructions, 736 -> 374 per wave, but each hop then waits ~3x longer: 80 vs 63 us per call,
+    // profiles/ab/r03i_pcap_uniform_walk.txt)
+    walk(lw, lbase, lst[w], base, entry, len, exit, cnt, err, rec);
     wave_lds_sync();
-    PCAP_STAMP(3);
-    store_region(S, k, list, rec, entry, exit, cnt, err);
-#if PKTGPU_STAMPS
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    PCAP_STAMP(4);
-    if (lane == 0 && g_pcap_stamps) {
-        uint32_t xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        for (int q = 0; q < 5; q++) g_pcap_stamps[(uint64_t)k * 8 + q] = pst[q];
-        g_pcap_stamps[(uint64_t)k * 8 + 6] = xcc & 15u;  // s_memtime counts per XCD
-    }
-#endif
-}
-
-// One block stages 4 consecutive regions (16 KiB + 16 B) and each wave guesses one of them.  (A
-// persistent form, each block looping over its tiles with the next tile's 16 KiB loaded into
-// registers during the current tile's walks, measured slower: 83 vs 61 us per C4 call — the
-// hardware already overlaps new blocks' staging with resident blocks' walks, round 3.)
-__global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len,
-                                                         uint32_t K, Scratch S) {
-    uint64_t pst[5] = {0, 0, 0, 0, 0};
-    (void)pst;
-    PCAP_STAMP(0);
-    __shared__ uint4 lds[kBlockBytes / 16 + 2];
-    __shared__ uint16_t lst[kWaves][kMaxRec];
-    const uint32_t w = threadIdx.x / 64;
-    const uint32_t k = blockIdx.x * kWaves + w;
-    const uint64_t lbase = (uint64_t)blockIdx.x * kBlockBytes;
-    stage<kBlockBytes, 256>(lds, buf, lbase, len, threadIdx.x);
-    // the per-call zeroing the repair rounds rely on (no memset launches): control words 1.. here,
-    // word 0 (the magic) and each region's owner word in guess_region
-    if (blockIdx.x == 0)
-        for (uint32_t c = 1 + threadIdx.x; c < kCtlWords; c += 256) S.ctl[c] = 0;
-    __syncthreads();
-    PCAP_STAMP(1);
-    if (k < K) guess_region(buf, len, K, S, reinterpret_cast<const uint32_t*>(lds), lst[w], lbase, k, pst);
-}
-
-// One repair round (see the file header).  `slot` = this round's two control words.
-__global__ __launch_bounds__(256) void pcap_repair_kernel(const uint8_t* __restrict__ buf, uint64_t len,
-                                                          uint32_t K, Scratch S, uint32_t slot, uint32_t round) {
-    __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
-    __shared__ uint16_t lst[kWaves][kMaxRec];
-    __shared__ uint32_t qk[256];
-    __shared__ uint64_t qe[256];
-    __shared__ uint32_t qn;
-    const uint32_t t = threadIdx.x, w = t / 64;
-    if (t == 0) qn = 0;
-    __syncthreads();
-    const uint32_t k = blockIdx.x * 256 + t;
-    if (k > 0 && k < K) {
-        const uint32_t j = left_of(S, k);
-        const uint64_t e = S.exit[j];
-        if (e != S.entry[k]) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[slot]), 1ull);
-            atomicMax(reinterpret_cast<unsigned long long*>(&S.ctl[slot + 1]), (unsigned long long)(K - k));
-            if ((j == 0 || S.exit[left_of(S, j)] == S.entry[j]) && e >= (uint64_t)k * kRegion) {
-                const uint32_t q = atomicAdd(&qn, 1u);
-                qk[q] = k;
-                qe[q] = e;
-            }
+    uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+    if (lane < cnt) dst[lane] = (uint16_t)rec;
+    for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = lst[w][i];
+    if (lane == 0) {
+        S.rentry[k] = entry;
+        S.rexit[k] = exit;
+        S.rcnt[k] = cnt | (err ? 0x80000000u : 0u);
+        if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
+            const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
+            __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+}
+
+// Block-wide exclusive composition of the threads' aggregates in thread order (all 256 threads).
+// Also returns `idx`: the thread index of the nearest claiming (non-none) aggregate before t, or -1.
+__device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, int32_t* widx, Agg& total) {
+    const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
+    int32_t ix = (a.bits & kBitNone) ? -1 : (int32_t)t;
+    Agg x = a;
+#pragma unroll
+    for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan within the wave
+        Agg y;
+        y.first = __shfl_up(x.first, d, 64);
+        y.last = __shfl_up(x.last, d, 64);
+        y.cnt = __shfl_up(x.cnt, d, 64);
+        y.bits = __shfl_up(x.bits, d, 64);
+        const int32_t iy = __shfl_up(ix, d, 64);
+        if (lane >= d) {
+            x = combine(y, x);
+            ix = ix >= 0 ? ix : iy;
+        }
+    }
+    if (lane == 63) {
+        wtot[w] = x;
+        widx[w] = ix;
+    }
     __syncthreads();
-    const uint32_t n = qn;
-    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds[w]);
-    for (uint32_t i = w; i < n; i += kWaves) {
-        uint32_t r = qk[i];
-        uint64_t e = qe[i];
-        for (int step = 0; step < kChaseMax; step++) {
-            // claim region r for this round; a region another chase claimed first is its alone
-            uint32_t prev = 0;
-            if (lane_id() == 0) prev = atomicMax(&S.own[r], round);
-            if (__shfl(prev, 0, 64) >= round) break;
-            const uint64_t base = (uint64_t)r * kRegion;
+    Agg before = agg_identity();
+    int32_t ib = -1;
+    for (uint32_t q = 0; q < w; q++) {
+        before = combine(before, wtot[q]);
+        ib = widx[q] >= 0 ? widx[q] : ib;
+    }
+    total = agg_identity();
+    for (uint32_t q = 0; q < (uint32_t)kWaves; q++) total = combine(total, wtot[q]);
+    // exclusive: the wave prefix before this lane
+    Agg ex;
+    ex.first = __shfl_up(x.first, 1, 64);
+    ex.last = __shfl_up(x.last, 1, 64);
+    ex.cnt = __shfl_up(x.cnt, 1, 64);
+    ex.bits = __shfl_up(x.bits, 1, 64);
+    int32_t iex = __shfl_up(ix, 1, 64);
+    if (lane == 0) {
+        ex = agg_identity();
+        iex = -1;
+    }
+    idx = iex >= 0 ? iex : ib;
+    __syncthreads();  // wtot / widx reusable
+    return combine(before, ex);
+}
+
+// Does a region with aggregate r disagree with the run `pre` before it (pre claiming)?
+__device__ __forceinline__ bool seam_bad(const Agg& pre, const Agg& r) {
+    if (pre.bits & kBitNone) return false;
+    return (r.bits & kBitNone) ? pre.last < r.last : pre.last != r.first;
+}
+
+// Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
+__global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
+                                                        uint32_t nb, int ticket, Scratch S) {
+    __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
+    __shared__ uint16_t lst[kWaves][kMaxRec];
+    __shared__ uint64_t sen[kScanRegions], sex[kScanRegions];
+    __shared__ uint32_t scw[kScanRegions];
+    __shared__ uint32_t fq[kScanRegions];
+    __shared__ uint64_t fe[kScanRegions];
+    __shared__ uint8_t sbad[kScanRegions];
+    __shared__ Agg wtot[kWaves];
+    __shared__ int32_t widx[kWaves];
+    __shared__ uint32_t s_blk, s_nf, s_retry, s_near, csum[kWaves];
+    __shared__ Agg s_P;
+    const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
+    // the block order: blockIdx when every block of the grid is resident at once (the host checks
+    // the occupancy), else a ticket (every lower block is then already running)
+    if (t == 0) s_blk = ticket ? atomicAdd(S.ticket, 1u) : blockIdx.x;
+    __syncthreads();
+    const uint32_t blk = s_blk;
+    const uint32_t k = blk * kScanRegions + t;
+    if (k < K) {
+        sen[t] = S.rentry[k];
+        sex[t] = S.rexit[k];
+        scw[t] = S.rcnt[k];
+    } else {
+        sen[t] = sex[t] = 0;
+        scw[t] = 0;
+    }
+    __syncthreads();
+    // Re-walk the queued regions fq[0, s_nf) from fe[]: one wave per region (stage its 4 KiB, walk),
+    // the state to LDS and global memory.
+    auto run_fixes = [&]() {
+        const uint32_t nf = s_nf;
+        for (uint32_t i = w; i < nf; i += kWaves) {
+            const uint32_t r = fq[i], kk = blk * kScanRegions + r;
+            const uint64_t base = (uint64_t)kk * kRegion, e = fe[i];
             wave_lds_sync();
-            if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane_id());
+            if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane);
             wave_lds_sync();
             uint64_t exit;
             uint32_t cnt, err, rec;
-            walk(lw, base, lst[w], base, e, len, exit, cnt, err, rec);
+            walk(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, exit, cnt, err, rec);
             wave_lds_sync();
-            store_region(S, r, lst[w], rec, e, exit, cnt, err);
-            e = exit;
-            if (++r >= K || e == S.entry[r] || e < (uint64_t)r * kRegion) break;
+            uint16_t* dst = S.list + (uint64_t)kk * kMaxRec;
+            if (lane < cnt) dst[lane] = (uint16_t)rec;
+            for (uint32_t j = 64 + lane; j < cnt; j += 64) dst[j] = lst[w][j];
+            if (lane == 0) {
+                const uint32_t cw = cnt | (err ? 0x80000000u : 0u);
+                sen[r] = e;
+                sex[r] = exit;
+                scw[r] = cw;
+                S.rentry[kk] = e;
+                S.rexit[kk] = exit;
+                S.rcnt[kk] = cw;
+            }
         }
+        __syncthreads();
+    };
+    // ---- local fixes: a region that disagrees with the claiming region before it (in this block)
+    // while that one agrees with its own left is re-walked from its exit; until no such region
+    Agg total;
+    for (;;) {
+        const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
+        int32_t j;
+        const Agg pre = block_exclusive(mine, j, wtot, widx, total);
+        const bool bad = j >= 0 && seam_bad(pre, mine);
+        sbad[t] = bad;
+        // (an exit landing before this region's start means a "none" region between is wrong: that
+        // one is fixed first, never this one from a position outside it)
+        if (t == 0) s_nf = 0;
+        __syncthreads();
+        if (bad && !sbad[j] && pre.last >= (uint64_t)k * kRegion) {
+            const uint32_t q = atomicAdd(&s_nf, 1u);
+            fq[q] = t;
+            fe[q] = pre.last;
+        }
+        __syncthreads();
+        if (s_nf == 0) break;
+        run_fixes();
+    }
+    // ---- publish the aggregate; compose the blocks before (stopping at the nearest exact one)
+    BlkDesc* my = S.blk + blk;
+    if (t == 0) {
+        st_agent(&my->a_first, total.first);
+        st_agent(&my->a_last, total.last);
+        st_agent(&my->a_cnt, total.cnt);
+        vm_drain();
+        st_agent(&my->a_meta, ((uint64_t)S.epoch << 8) | kPublished | total.bits);
+    }
+    Agg P = agg_identity();
+    for (;;) {
+        Agg acc = agg_identity();
+        bool exact = blk == 0;
+        uint64_t il = 0, ic = 0;
+        uint32_t ib = 0;
+        if (t == 0) s_retry = 0;
+        for (int64_t hi = blk; hi > 0 && !exact;) {
+            // window [hi - 256, hi): lane l of wave v reads block hi - 1 - 64 v - l
+            const int64_t jj = hi - 1 - (int64_t)t;
+            uint32_t st = 0;  // 0 unpublished, 1 aggregate, 2 exact
+            Agg a = agg_identity();
+            uint64_t xl = 0, xc = 0, xm = 0;
+            if (jj >= 0) {
+                const BlkDesc* d = S.blk + jj;
+                const uint64_t im = ld_agent(&d->i_meta), am = ld_agent(&d->a_meta);
+                vm_drain();
+                if ((uint32_t)(im >> 8) == S.epoch) {
+                    st = 2;
+                    xl = ld_agent(&d->i_last);
+                    xc = ld_agent(&d->i_cnt);
+                    xm = im;
+                } else if ((uint32_t)(am >> 8) == S.epoch) {
+                    st = 1;
+                    a = Agg{ld_agent(&d->a_first), ld_agent(&d->a_last), ld_agent(&d->a_cnt), (uint32_t)am & 15u};
+                }
+            }
+            // the nearest exact block in the window (the smallest thread index with st == 2)
+            if (t == 0) s_near = 256;
+            __syncthreads();
+            if (st == 2) atomicMin(&s_near, t);
+            __syncthreads();
+            const uint32_t near = s_near;
+            if (jj >= 0 && t < near && st == 0) s_retry = 1;  // a nearer block has not published
+            if (t >= near) a = agg_identity();
+            // compose the window's aggregates after the nearest exact block in block order: thread
+            // order is reversed block order — within a wave lane 63 is the earliest, and wave 3 the
+            // earliest wave
+            Agg wr = agg_identity();
+            {
+                Agg x = a;
+#pragma unroll
+                for (uint32_t dd = 1; dd < 64; dd <<= 1) {
+                    Agg y;
+                    y.first = __shfl_down(x.first, dd, 64);
+                    y.last = __shfl_down(x.last, dd, 64);
+                    y.cnt = __shfl_down(x.cnt, dd, 64);
+                    y.bits = __shfl_down(x.bits, dd, 64);
+                    if (lane + dd >= 64) y = agg_identity();
+                    x = combine(y, x);
+                }
+                if (lane == 0) wtot[w] = x;
+                __syncthreads();
+                for (int q = kWaves - 1; q >= 0; q--) wr = combine(wr, wtot[q]);
+                __syncthreads();
+            }
+            acc = combine(wr, acc);
+            if (near < 256) {
+                exact = true;
+                if (t == near) {
+                    s_P = Agg{0, xl, xc, (uint32_t)xm & kBitErr};
+                }
+                __syncthreads();
+                il = s_P.last;
+                ic = s_P.cnt;
+                ib = s_P.bits;
+                __syncthreads();
+            }
+            hi -= 256;
+            if (s_retry) break;
+        }
+        __syncthreads();
+        if (s_retry || !exact) {  // a block before has not published, or none is exact yet
+            __builtin_amdgcn_s_sleep(8);
+            continue;
+        }
+        if (blk == 0) {
+            P = agg_identity();
+            break;
+        }
+        // P = the exact state before this block: (exit, count, error)
+        if (acc.bits & kBitNone) {
+            if (il >= acc.last) {
+                P = Agg{0, il, ic, ib | 0u};
+                break;
+            }
+        } else if (!(acc.bits & kBitBad) && acc.first == il) {
+            P = Agg{0, acc.last, ic + acc.cnt, ib | (acc.bits & kBitErr)};
+            break;
+        }
+        __builtin_amdgcn_s_sleep(8);  // an earlier block has not fixed its first seam yet
+    }
+    // ---- this block's seams against the exact exit before it: fix the first disagreeing region
+    // from the exact state before it, until none disagrees (exact by induction)
+    Agg exact_pre = blk == 0 ? agg_identity() : Agg{P.last, P.last, 0, 0};  // "claims" the exact exit
+    for (;;) {
+        const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
+        int32_t j;
+        const Agg pre0 = block_exclusive(mine, j, wtot, widx, total);
+        const Agg pre = combine(exact_pre, pre0);
+        const bool bad = seam_bad(pre, mine) && !(pre.bits & kBitBad) && pre.last >= (uint64_t)k * kRegion;
+        if (t == 0) s_nf = 0;
+        __syncthreads();
+        if (bad) {  // exactly one region: the first disagreeing seam
+            fq[0] = t;
+            fe[0] = pre.last;
+            s_nf = 1;
+        }
+        __syncthreads();
+        if (s_nf == 0) break;
+        run_fixes();
+    }
+    // ---- the exact state after this block; each region's record prefix
+    const Agg all = combine(blk == 0 ? agg_identity() : Agg{P.last, P.last, 0, 0}, total);
+    const uint64_t c_before = blk == 0 ? 0 : P.cnt;
+    const uint32_t err_all = (P.bits | all.bits) & kBitErr;
+    const uint64_t last = (all.bits & kBitNone) ? P.last : all.last;
+    if (t == 0) {
+        st_agent(&my->i_last, last);
+        st_agent(&my->i_cnt, c_before + total.cnt);
+        vm_drain();
+        st_agent(&my->i_meta, ((uint64_t)S.epoch << 8) | kPublished | err_all);
+        if (blk == nb - 1) {
+            __hip_atomic_store(&S.host[kHostTotal], c_before + total.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err_all ? 1 : 0), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    {
+        uint32_t x = k < K ? (scw[t] & 0x7FFFFFFFu) : 0u, c = x;
+#pragma unroll
+        for (uint32_t d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= d) x += y;
+        }
+        if (lane == 63) csum[w] = x;
+        __syncthreads();
+        uint64_t before = c_before;
+        for (uint32_t q = 0; q < w; q++) before += csum[q];
+        if (k < K) S.rpre[k] = before + x - c;
     }
 }
 
-// Exclusive prefix of cnt within each block of kScanBlock regions (256 threads x 4), the block
-// totals to bpre, and the OR of the regions' error flags.  The last block to finish (ticket in
-// ctl[slot + 2]) then scans the block totals in place and writes the record total to
-// ctl[slot + 1]; ctl[slot] collects the error flags.
-__global__ __launch_bounds__(256) void pcap_scan_kernel(uint32_t K, uint32_t nb, Scratch S, uint32_t slot,
-                                                        uint32_t pass_slot, uint64_t* host_ctl) {
-    __shared__ uint64_t wsum[4];
-    __shared__ uint64_t carry;
-    __shared__ uint32_t last;
-    const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const uint32_t k0 = blockIdx.x * kScanBlock + t * 4;
-    uint32_t c[4], e = 0, s = 0;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        c[i] = k0 + i < K ? S.cnt[k0 + i] : 0;
-        e |= k0 + i < K ? S.err[k0 + i] : 0;
-        s += c[i];
-    }
-    if (__ballot(e != 0) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(&S.ctl[slot]), 1ull);
-    uint32_t x = s;  // inclusive wave scan
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        if (lane >= (uint32_t)d) x += y;
-    }
-    if (lane == 63) wsum[w] = x;
-    __syncthreads();
-    uint32_t wbase = 0;
-    for (uint32_t i = 0; i < w; i++) wbase += (uint32_t)wsum[i];
-    uint32_t run = wbase + x - s;
-#pragma unroll
-    for (int i = 0; i < 4; i++) {
-        if (k0 + i < K) S.pre[k0 + i] = run;
-        run += c[i];
-    }
-    if (t == 255) S.bpre[blockIdx.x] = (uint64_t)wbase + x;
-    __threadfence();
-    __syncthreads();
-    if (t == 0) last = atomicAdd(reinterpret_cast<unsigned long long*>(&S.ctl[slot + 2]), 1ull) == nb - 1;
-    __syncthreads();
-    if (!last) return;
-    // Last block: exclusive scan of the block totals (read past L1: other blocks wrote them).
-    __threadfence();
-    if (t == 0) carry = 0;
-    __syncthreads();
-    for (uint32_t b0 = 0; b0 < nb; b0 += 256) {
-        const uint32_t b = b0 + t;
-        const uint64_t v = b < nb ? __hip_atomic_load(&S.bpre[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-        uint64_t y = v;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint64_t z = __shfl_up(y, d, 64);
-            if (lane >= (uint32_t)d) y += z;
-        }
-        __syncthreads();
-        if (lane == 63) wsum[w] = y;
-        __syncthreads();
-        uint64_t wb = carry;
-        for (uint32_t i = 0; i < w; i++) wb += wsum[i];
-        if (b < nb) S.bpre[b] = wb + y - v;
-        __syncthreads();
-        if (t == 255) carry = wb + y;
-        __syncthreads();
-    }
-    if (t == 0) S.ctl[slot + 1] = carry;
-    // The pass's verdict to the host's pinned words directly (no copy launch): the magic word and
-    // the pass's 8 control words (the repair rounds' counts, this kernel's error flag and total).
-    __syncthreads();
-    if (t < 9) {
-        const uint32_t wi = t == 0 ? 0u : pass_slot + t - 1;
-        const uint64_t v = wi == slot + 1 ? carry : __hip_atomic_load(&S.ctl[wi], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(&host_ctl[wi], v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-}
-
-// 256 threads write the records of kEmitRegions consecutive regions, one record per thread per
-// step, contiguous in the output (coalesced), at the regions' scanned prefix.
+// Emit (file header: EMIT): 256 threads write the records of 16 consecutive regions, one record per
+// thread per step, contiguous in the output (coalesced), at the regions' exact prefix.
 __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
                                                         uint64_t* __restrict__ offsets,
                                                         uint32_t* __restrict__ lens) {
     __shared__ uint32_t cpre[kEmitRegions + 1];
     const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
     if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
-        const uint32_t c = t < kEmitRegions && k0 + t < K ? S.cnt[k0 + t] : 0;
+        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & 0x7FFFFFFFu) : 0;
         uint32_t x = c;
 #pragma unroll
         for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
@@ -514,7 +657,7 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
         if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
     }
     __syncthreads();
-    const uint64_t first = (uint64_t)S.pre[k0] + S.bpre[k0 / kScanBlock];
+    const uint64_t first = S.rpre[k0];
     const uint32_t total = cpre[kEmitRegions];
     for (uint32_t i = t; i < total; i += 256) {
         const uint64_t idx = first + i;
@@ -527,7 +670,7 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
         const uint64_t base = (uint64_t)k * kRegion;
         const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
         const uint64_t pos = base + list[li];
-        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.exit[k];
+        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.rexit[k];
         offsets[idx] = pos + 16;
         lens[idx] = (uint32_t)(next - pos - 16);
     }
@@ -536,13 +679,6 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
 }  // namespace
 
 extern "C" {
-#if PKTGPU_STAMPS
-// Diagnostic build only: where pcap_guess_kernel writes its per-wave stamps (8 u64 per region).
-int pkt_debug_pcap_stamps(void* dev_buf) {
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_pcap_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? PKT_SUCCESS
-                                                                                            : PKT_ERR_HIP;
-}
-#endif
 
 int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                           uint64_t cap, uint64_t* n_out, void* stream) {
@@ -552,13 +688,13 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
     const uint64_t K64 = (len + kRegion - 1) / kRegion;
     if (K64 > (1ull << 31)) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
-    const uint32_t K = (uint32_t)K64, nb = (K + kScanBlock - 1) / kScanBlock;
+    const uint32_t K = (uint32_t)K64, nb = (K + kScanRegions - 1) / kScanRegions;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
-    // Scratch: the control words, per-region words and record lists, the scan-block prefixes.
-    const uint64_t need = 8ull * kCtlWords + (uint64_t)K * (8 + 8 + 4 + 4 + 4 + 4 + 2 * kMaxRec) + 8ull * nb + 64;
+    // Scratch: the ticket, the scan blocks' states, per-region states, prefixes and record lists.
+    const uint64_t need = 64 + (uint64_t)nb * sizeof(BlkDesc) + (uint64_t)K * (8 + 8 + 8 + 4 + 2 * kMaxRec);
     PcapScratch& pc = ctx->pc;
     if (pc.bytes < need) {
         if (pc.buf) {
@@ -567,67 +703,60 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
             pc.buf = nullptr;
             pc.bytes = 0;
         }
-        e = hipMalloc(&pc.buf, need + need / 4);
+        const uint64_t bytes = need + need / 4;
+        e = hipMalloc(&pc.buf, bytes);
+        if (e == hipSuccess) e = hipMemsetAsync(pc.buf, 0, bytes, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
-        pc.bytes = need + need / 4;
+        pc.bytes = bytes;
     }
     if (!pc.ctl) {
-        e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kCtlWords, hipHostMallocMapped);
+        e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kHostWords, hipHostMallocMapped);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&pc.ctl_dev), pc.ctl, 0);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc (pcap index)");
     }
+    // a new epoch per call (block states of older calls are ignored, not cleared; they may lie
+    // anywhere in the buffer, hence the full reset on wrap)
+    if (++pc.epoch >= (1u << 24)) {
+        pc.epoch = 1;
+        if ((e = hipMemsetAsync(pc.buf, 0, pc.bytes, s)) != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
+    }
     Scratch S;
     char* p = static_cast<char*>(pc.buf);
-    S.ctl = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * kCtlWords;
-    S.entry = reinterpret_cast<uint64_t*>(p);
+    S.ticket = reinterpret_cast<uint32_t*>(p);
+    S.blk = reinterpret_cast<BlkDesc*>(p + 64);
+    p += 64 + (uint64_t)nb * sizeof(BlkDesc);
+    S.rentry = reinterpret_cast<uint64_t*>(p);
     p += 8ull * K;
-    S.exit = reinterpret_cast<uint64_t*>(p);
+    S.rexit = reinterpret_cast<uint64_t*>(p);
     p += 8ull * K;
-    S.bpre = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * nb;
-    S.cnt = reinterpret_cast<uint32_t*>(p);
-    p += 4ull * K;
-    S.err = reinterpret_cast<uint32_t*>(p);
-    p += 4ull * K;
-    S.pre = reinterpret_cast<uint32_t*>(p);
-    p += 4ull * K;
-    S.own = reinterpret_cast<uint32_t*>(p);
+    S.rpre = reinterpret_cast<uint64_t*>(p);
+    p += 8ull * K;
+    S.rcnt = reinterpret_cast<uint32_t*>(p);
     p += 4ull * K;
     S.list = reinterpret_cast<uint16_t*>(p);
-
+    S.host = pc.ctl_dev;
+    S.epoch = pc.epoch;
+    for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
-    // (the guess kernel zeroes the control words and the owner words)
     hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
-    if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap guess launch");
-    // Each pass: two repair rounds, then the scan and the emit on speculation, and ONE read-back.
-    // When the second round found no region disagreeing, the state it saw was the fixed point and
-    // the emitted index is final; otherwise the pass repeats (every round fixes at least the
-    // first wrong region, so K passes always suffice).
-    for (uint32_t pass = 0;; pass++) {
-        if (pass > K) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap index did not converge");
-        const uint32_t slot = 8 + 8 * (pass % kPassSlots);
-        if (pass && pass % kPassSlots == 0) {
-            e = hipMemsetAsync(S.ctl + 8, 0, 8ull * (kCtlWords - 8), s);
-            if (e != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
-        }
-        for (uint32_t r = 0; r < kRounds; r++)  // round ids 1, 2, 3, ... (owner words start at 0)
-            hipLaunchKernelGGL(pcap_repair_kernel, dim3((K + 255) / 256), blk, 0, s, buf, len, K, S, slot + 2 * r,
-                               kRounds * pass + r + 1);
-        hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, K, nb, S, slot + 4, slot, pc.ctl_dev);
-        if (cap)
-            hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap,
-                               S, offsets, lens);
-        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
-        e = hipStreamSynchronize(s);
-        if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
-        if (!pc.ctl[0]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
-        if (pc.ctl[slot + 2 * (kRounds - 1)] == 0) {
-            if (pc.ctl[slot + 4]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
-            *n_out = pc.ctl[slot + 5];
-            return PKT_SUCCESS;
-        }
+    if (!pc.scan_resident) {  // scan blocks the device holds at once
+        int per_cu = 0, cus = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_scan_kernel, 256, 0) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+            per_cu = cus = 0;
+        pc.scan_resident = (uint32_t)std::max(1, per_cu * cus);
     }
+    // (tickets serialise: 186 device-scope atomics on one word cost the last block ~2.4 us)
+    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
+    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipMemsetAsync(S.ticket, 0, 4, s);  // the next call's tickets start at 0
+    if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
+    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "pcap index");
+    if (!pc.ctl[kHostMagic]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
+    if (pc.ctl[kHostErr]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
+    *n_out = pc.ctl[kHostTotal];
+    return PKT_SUCCESS;
 }
 
 }  // extern "C"

@@ -8,7 +8,7 @@
 // the same per-lane store widths — but no walk and no field logic: every stored value is a cheap
 // mix of the loaded words.  Its launch time is what ANY kernel with C2's traffic shape costs in
 // one launch on this box, so parse / ceiling says how much of the gap to the HBM peak is the
-// parser's own.
+// parser's own.  pkt_probe_ceiling_groups: the same for the C3 column set (bench.py --config c3).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -64,7 +64,91 @@ __global__ __launch_bounds__(256) void ceiling_kernel(const uint8_t* slab, uint3
     put<uint16_t>(o.udp_checksum, i, (uint16_t)(c.y >> 16));
 }
 
+// The C3 form (pkt_probe_ceiling_groups): the same loads, and stores into EVERY requested column of
+// the chain (`slots` header slots), Ether, Vlan, IPv4, TCP and UDP groups with the parse's widths
+// (a group is written when its first column is non-NULL; the parse writes absent groups as zeros).
+__global__ __launch_bounds__(256) void ceiling_groups_kernel(const uint8_t* slab, uint32_t n, uint32_t stride,
+                                                             uint32_t slots, pkt_out_t o) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= n) return;
+    const uint4* p = reinterpret_cast<const uint4*>(slab + (uint64_t)i * stride);
+    const uint4 a = p[0], b = p[1], c = p[2], d = p[3];
+    const uint32_t v0 = a.x ^ d.w, v1 = a.y ^ c.z, v2 = a.z ^ b.y, v3 = a.w ^ c.x;
+    const uint32_t v4 = b.x ^ d.x, v5 = b.z ^ c.y, v6 = b.w ^ d.y, v7 = c.w ^ d.z;
+    put<uint8_t>(o.status, i, (uint8_t)(v0 & 1));
+    put<uint8_t>(o.n_hdrs, i, (uint8_t)(3 + (v1 & 1)));
+    for (uint32_t j = 0; j < slots; j++) {
+        put<uint8_t>(o.hdr_type, j * n + i, (uint8_t)(v2 >> (8 * (j & 3))));
+        put<uint16_t>(o.hdr_off, j * n + i, (uint16_t)(v3 >> (5 * (j & 3))));
+    }
+    put<uint16_t>(o.payload_off, i, (uint16_t)v4);
+    put<uint16_t>(o.payload_len, i, (uint16_t)(v4 >> 16));
+    put<uint32_t>(o.hdr_mask, i, v5);
+    if (o.eth_dst) {
+        put<uint64_t>(o.eth_dst, i, ((uint64_t)a.x << 16) | (a.y >> 16));
+        put<uint64_t>(o.eth_src, i, ((uint64_t)a.y << 32) | a.z);
+        put<uint16_t>(o.eth_etype, i, (uint16_t)a.w);
+    }
+    if (o.vlan_pcp) {
+        put<uint8_t>(o.vlan_pcp, i, (uint8_t)(b.x >> 29));
+        put<uint8_t>(o.vlan_cfi, i, (uint8_t)(b.x >> 28));
+        put<uint16_t>(o.vlan_vid, i, (uint16_t)(b.x >> 16));
+        put<uint16_t>(o.vlan_etype, i, (uint16_t)b.x);
+    }
+    if (o.ipv4_version) {
+        put<uint8_t>(o.ipv4_version, i, (uint8_t)(v6 >> 4));
+        put<uint8_t>(o.ipv4_ihl, i, (uint8_t)v6);
+        put<uint8_t>(o.ipv4_diffserv, i, (uint8_t)(v6 >> 8));
+        put<uint16_t>(o.ipv4_total_len, i, (uint16_t)(v6 >> 16));
+        put<uint16_t>(o.ipv4_identification, i, (uint16_t)v7);
+        put<uint8_t>(o.ipv4_flags, i, (uint8_t)(v7 >> 29));
+        put<uint16_t>(o.ipv4_frag_startset, i, (uint16_t)(v7 >> 16));
+        put<uint8_t>(o.ipv4_ttl, i, (uint8_t)(b.x >> 8));
+        put<uint8_t>(o.ipv4_protocol, i, (uint8_t)b.x);
+        put<uint16_t>(o.ipv4_header_checksum, i, (uint16_t)(b.y >> 16));
+        put<uint32_t>(o.ipv4_src, i, b.z);
+        put<uint32_t>(o.ipv4_dst, i, b.w);
+        put<uint16_t>(o.ipv4_csum_calc, i, (uint16_t)(v0 + v1 + v2 + v3));
+    }
+    if (o.tcp_src) {
+        put<uint16_t>(o.tcp_src, i, (uint16_t)c.z);
+        put<uint16_t>(o.tcp_dst, i, (uint16_t)(c.z >> 16));
+        put<uint32_t>(o.tcp_seq_no, i, c.w ^ v0);
+        put<uint32_t>(o.tcp_ack_no, i, d.x ^ v1);
+        put<uint8_t>(o.tcp_data_startset, i, (uint8_t)(d.y >> 28));
+        put<uint8_t>(o.tcp_res, i, (uint8_t)(d.y >> 24));
+        put<uint8_t>(o.tcp_flags, i, (uint8_t)(d.y >> 16));
+        put<uint16_t>(o.tcp_window, i, (uint16_t)d.y);
+        put<uint16_t>(o.tcp_checksum, i, (uint16_t)(d.z >> 16));
+        put<uint16_t>(o.tcp_urgent_ptr, i, (uint16_t)d.z);
+    }
+    if (o.udp_src) {
+        put<uint16_t>(o.udp_src, i, (uint16_t)c.x);
+        put<uint16_t>(o.udp_dst, i, (uint16_t)(c.x >> 16));
+        put<uint16_t>(o.udp_length, i, (uint16_t)c.y);
+        put<uint16_t>(o.udp_checksum, i, (uint16_t)(c.y >> 16));
+    }
+}
+
 }  // namespace
+
+extern "C" int pkt_probe_ceiling_groups(const uint8_t* slab, uint64_t n, uint32_t stride, uint32_t slots,
+                                        const pkt_out_t* out, void* stream) {
+    // every column of each written group present (chain always; a group by its first column)
+    if (!slab || !out || n == 0 || n >= (1ull << 26) || stride < 64 || (stride & 15) || slots > PKT_MAX_HDRS)
+        return PKT_ERR_INVALID_ARG;
+    const void* const* cols = reinterpret_cast<const void* const*>(out);
+    static const int lo[7] = {0, 7, 10, 14, 27, 35, 45}, hi[7] = {7, 10, 14, 27, 35, 45, 49};
+    for (int g = 0; g < 7; g++) {
+        if (g == 4 && cols[lo[g]]) return PKT_ERR_INVALID_ARG;  // IPv6: not part of any probe shape
+        if (g > 0 && !cols[lo[g]]) continue;
+        for (int c = lo[g]; c < hi[g]; c++)
+            if (!cols[c]) return PKT_ERR_INVALID_ARG;
+    }
+    hipLaunchKernelGGL(ceiling_groups_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                       reinterpret_cast<hipStream_t>(stream), slab, (uint32_t)n, stride, slots, *out);
+    return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
+}
 
 extern "C" int pkt_probe_ceiling(const uint8_t* slab, uint64_t n, uint32_t stride, const pkt_out_t* out,
                                  void* stream) {

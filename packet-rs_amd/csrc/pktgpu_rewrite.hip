@@ -443,7 +443,8 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
             locate(g, ca, lo, hi, o);
             put(ca, lo, hi, o);
         }
-    } else {  // C4: 142 vs 148 us in the input's layout, 124 vs 138 us packed
+    } else {  // C4: 142 vs 148 us in the input's layout, 124 vs 138 us packed (two rounds ahead:
+              // 141 / 108 vs 142 / 105 us, round 3, profiles/ab/r03g_to_vec_lookahead2.txt)
         uint64_t ca = 0, lo = 0, hi = 0;
         uint32_t o[4] = {0, 0, 0, 0};
         locate(lane, ca, lo, hi, o);  // lane < 256 < total

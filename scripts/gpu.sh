@@ -58,8 +58,7 @@ for step in "$@"; do
            python scripts/pmc_summary.py gpurun_out/${TAG}_$n > "$OUT/$n.txt"; cat "$OUT/$n.txt" ;;
     stamps) run stamps 600 bash -c 'export PKTGPU_LIB=packet-rs_amd/lib/variants/stamps.so;
                for s in "c4 all 64" "c4 all 128"; do
-                 set -- $s; python scripts/stamps.py --config $1 --columns $2 --window $3 || exit $?; done
-               python scripts/stamps_pcap.py' ;;
+                 set -- $s; python scripts/stamps.py --config $1 --columns $2 --window $3 || exit $?; done' ;;
     pcapab) run pcapab 900 bash -c 'for rep in 1 2 3; do for v in packet-rs_amd/lib/variants/*.so; do
                PKTGPU_LIB=$v python scripts/pcap_index_bench.py --reps 20 | sed "s|^|$(basename $v) |" || exit $?; done; done' ;;
     pcap)  run pcap 300 python scripts/pcap_index_bench.py --reps 20

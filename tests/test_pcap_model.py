@@ -1,8 +1,8 @@
-"""CPU model of the device pcap indexer's speculation + fix-up (pktgpu_pcap.hip): the same
-regions, plausibility guess, per-region walk and repair rounds (each round reading the state the
-round started from — one legal interleaving of the kernel's waves), checked against the host
-indexer on captures built to make the guess wrong.  This pins the algorithm's exactness claim
-without a GPU; tests/test_pcap_device.py checks the kernels themselves."""
+"""CPU model of the device pcap indexer's speculation + exact scan (pktgpu_pcap.hip): the same
+regions, plausibility guess, per-region walk, state composition, local fix rounds, look-back
+(from random earlier exact blocks: legal interleavings of the kernel's blocks) and fixes from the
+exact exit, checked against the host indexer on captures built to make the guess wrong.  This pins
+the algorithm's exactness claim without a GPU; tests/test_pcap_device.py checks the kernels themselves."""
 import struct
 
 import numpy as np
@@ -10,7 +10,6 @@ import numpy as np
 from pktgpu import gen
 
 R = 4096
-LOOKBACK = 64
 
 
 def u32(b, o):
@@ -20,7 +19,6 @@ def u32(b, o):
 
 MIN_HOPS = 2  # PKTGPU_PCAP_HOPS (pktgpu_pcap.hip)
 MAX_HOPS = 2
-CHASE_MAX = 256
 ORIG_MAX = 1 << 20
 TS_SPAN = 86400
 
@@ -63,13 +61,16 @@ def walk(b, base, entry):
     return pos, lst, err
 
 
+TILE = 4  # regions per guess block (staged together, pcap_guess_kernel)
+
+
 def guess(b, k, snap):
     """First candidate of the region, 64 offsets per step: the lowest whose chain checks out in
-    the block's staged bytes (4 regions + 16 B), else the lowest that checks out with reads past
+    the tile's staged bytes (TILE regions + 16 B), else the lowest that checks out with reads past
     them; none in the region -> "no record starts here"."""
     base = k * R
     stop = min(len(b), base + R)
-    lend = (k // 4 + 1) * 4 * R
+    lend = (k // TILE + 1) * TILE * R
     for c0 in range(base, stop, 64):
         cs = [c for c in range(c0, min(c0 + 64, stop)) if c + 16 <= len(b)]
         rs = [chain_ok(b, c, stop, snap, lend) for c in cs]
@@ -82,70 +83,129 @@ def guess(b, k, snap):
     return base + R
 
 
-def model_index(b, inject=None, order_seed=None):
-    """`inject` {region: entry} overrides the guess (adversarial wrong guesses); `order_seed`
-    runs each round's chases in a random order instead of queue order.  A chase claims every
-    region it rewrites for the round and stops at one another chase claimed first (the owner
-    words of pcap_repair_kernel), so each region's words come from one walk."""
+B = 256  # regions per scan block (pcap_scan_kernel)
+
+
+def combine(a, b):
+    """The state composition of pktgpu_pcap.hip (run a, then run b).  An aggregate is ("none",
+    end) — no region claims a record start, consistent with a predecessor exit >= end — or
+    (first, last, cnt, err, bad)."""
+    if a[0] == "none":
+        return ("none", max(a[1], b[1])) if b[0] == "none" else b
+    if b[0] == "none":
+        return (a[0], a[1], a[2], a[3], a[4] or a[1] < b[1])
+    return (a[0], b[1], a[2] + b[2], a[3] or b[3], a[4] or b[4] or a[1] != b[0])
+
+
+IDENT = ("none", 0)
+
+
+def region_agg(k, st):
+    entry, (ex, lst, err) = st
+    if k != 0 and entry >= (k + 1) * R:
+        return ("none", (k + 1) * R)
+    return (entry, ex, len(lst), bool(err), False)
+
+
+def seam_bad(pre, r):
+    if pre[0] == "none":
+        return False
+    return pre[1] < r[1] if r[0] == "none" else pre[1] != r[0]
+
+
+def model_index(b, inject=None, order_seed=None, block=B):
+    """The three kernels restated: per-region guesses (`inject` {region: entry} overrides them:
+    adversarial wrong guesses) and walks; per scan block of B regions the local fix rounds (a
+    region disagreeing with the claiming region before it, while that one agrees with its own
+    left, re-walks from its exit), the look-back — the block's exact prefix composed from the
+    published aggregates back to a RANDOM earlier exact block (one legal interleaving per
+    `order_seed`; the kernel stops at the nearest one) — and the fixes from the exact exit.
+    `block` < B exercises many scan blocks on small captures.
+    Asserts that every composition the kernel accepts gives the exact exit and count.  Returns
+    (offsets, lens, regions re-walked)."""
     b = bytes(b)
     snap = u32(b, 16) or (1 << 30)
     K = (len(b) + R - 1) // R
-    entry = [24 if k == 0 else guess(b, k, snap) for k in range(K)]
-    for k, e in (inject or {}).items():
-        if 0 < k < K:
-            entry[k] = e
-    rng = np.random.default_rng(order_seed) if order_seed is not None else None
-    state = [walk(b, k * R, entry[k]) for k in range(K)]
-    rounds = 0
-    while True:
-        rounds += 1
-        assert rounds <= K + 1
-        old_entry, old_state = list(entry), list(state)
-        changed = 0
-        def left(k):  # nearest region left of k that claims a record start (or region 0)
-            j, s = k - 1, 0
-            while s < LOOKBACK and j > 0 and old_entry[j] >= (j + 1) * R:
-                j -= 1
-                s += 1
-            return j
+    NB = (K + block - 1) // block
+    rng = np.random.default_rng(order_seed if order_seed is not None else 0)
+    st = []
+    for k in range(K):  # the guess kernel: every region guesses its own entry
+        e = 24 if k == 0 else (inject or {}).get(k, guess(b, k, snap))
+        st.append((e, walk(b, k * R, e)))
+    fixed = 0
 
-        queue = []
-        for k in range(1, K):
-            j = left(k)
-            e = old_state[j][0]
-            if e == old_entry[k]:
-                continue
-            changed += 1
-            # only a region whose left neighbour is settled (agrees with its own left) repairs,
-            # and then chases on through the following regions until an exit meets a stored entry
-            if (j == 0 or old_state[left(j)][0] == old_entry[j]) and e >= k * R:
-                queue.append((k, e))
-        if rng is not None:
-            queue = [queue[i] for i in rng.permutation(len(queue))]
-        owned = set()
-        for k, e in queue:  # one interleaving of the chasing waves
-            for _ in range(CHASE_MAX):
-                if k in owned:  # claimed by another chase this round
+    def local_fixes(lo, hi):
+        nonlocal fixed
+        while True:
+            pre, last_claim, bad = IDENT, -1, {}
+            queue = []
+            for k in range(lo, hi):
+                r = region_agg(k, st[k])
+                bad[k] = last_claim >= 0 and seam_bad(pre, r)
+                if bad[k] and not bad[last_claim] and pre[1] >= k * R:
+                    queue.append((k, pre[1]))
+                if r[0] != "none":
+                    last_claim = k
+                pre = combine(pre, r)
+            if not queue:
+                return pre
+            for k, e in queue:  # the waves of one round, from the states the round started with
+                st[k] = (e, walk(b, k * R, e))
+                fixed += 1
+
+    aggs = [local_fixes(q * block, min(K, (q + 1) * block)) for q in range(NB)]
+    incl = []  # exact (exit, count, err) after each block
+    for q in range(NB):
+        lo, hi = q * block, min(K, (q + 1) * block)
+        if q > 0:
+            E, C, err = incl[q - 1]
+            j = int(rng.integers(0, q))  # a look-back from exact block j through aggregates j+1..q-1
+            acc = IDENT
+            for x in range(j + 1, q):
+                acc = combine(acc, aggs[x])
+            e0, c0, r0 = incl[j]
+            if acc[0] == "none":
+                ok, got = e0 >= acc[1], (e0, c0, r0)
+            else:
+                ok, got = (not acc[4]) and acc[0] == e0, (acc[1], c0 + acc[2], r0 or acc[3])
+            if ok:
+                assert got == (E, C, err), (q, j)
+            pre0 = (E, E, 0, False, False)
+        else:
+            E, C, err = 24, 0, False
+            pre0 = IDENT
+        while True:  # the first disagreeing seam against the exact exit, until none
+            pre, todo = pre0, None
+            for k in range(lo, hi):
+                r = region_agg(k, st[k])
+                if seam_bad(pre, r) and not pre[4]:
+                    assert pre[1] >= k * R
+                    todo = (k, pre[1])
                     break
-                owned.add(k)
-                entry[k] = e
-                state[k] = walk(b, k * R, e)
-                e = state[k][0]
-                k += 1
-                if k >= K or e == entry[k] or e < k * R:
-                    break
-        if not changed:
-            break
-    if any(st[2] for st in state):
+                pre = combine(pre, r)
+            if todo is None:
+                break
+            st[todo[0]] = (todo[1], walk(b, todo[0] * R, todo[1]))
+            fixed += 1
+        tot = IDENT
+        for k in range(lo, hi):
+            tot = combine(tot, region_agg(k, st[k]))
+        aggs[q] = tot
+        if tot[0] == "none":
+            incl.append((E, C, err))
+        else:
+            incl.append((tot[1], C + tot[2], err or tot[3]))
+    if incl[-1][2]:
         raise ValueError("truncated pcap record")
     offs, lens = [], []
     for k in range(K):
-        ex, lst, _ = state[k]
+        _, (ex, lst, _) = st[k]
         for i, p in enumerate(lst):
             nxt = lst[i + 1] if i + 1 < len(lst) else ex
             offs.append(p + 16)
             lens.append(nxt - p - 16)
-    return np.array(offs, np.uint64), np.array(lens, np.uint32), rounds
+    assert len(offs) == incl[-1][1]
+    return np.array(offs, np.uint64), np.array(lens, np.uint32), fixed
 
 
 def records(pays, ts=None):
@@ -163,10 +223,10 @@ def check(b, **kw):
     return rounds
 
 
-def test_model_c4_isolated_wrong_guesses_cost_one_round():
+def test_model_c4_wrong_guesses_are_rare():
     for seed in (1, 2, 3):
         buf, _, _ = gen.gen_c4(4000, seed=seed)
-        assert check(buf.tobytes()) <= 2
+        assert check(buf.tobytes(), order_seed=seed) <= 6
 
 
 def test_model_fake_chains_and_large_records():
@@ -187,7 +247,8 @@ def test_model_fake_chains_and_large_records():
         else:
             pays.append(rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes())
     ts = [(0, int(rng.integers(0, 2 * 10**6))) for _ in pays]
-    print("rounds", check(records(pays, ts)))
+    for order in range(4):
+        print("regions re-walked", check(records(pays, ts), order_seed=order))
 
 
 def test_model_errors_and_tails():
@@ -202,8 +263,9 @@ def test_model_errors_and_tails():
 
 
 def test_model_adjacent_wrong_guesses_any_chase_order():
-    """Wrong guesses in regions a and a+2 (and runs of them), chases in random orders: the
-    ownership rule keeps every region consistent and the fixed point exact."""
+    """Wrong guesses in regions a and a+2 (and runs of them), look-backs from random exact
+    blocks: every composition that checks out is exact, and the fixes give the host indexer's
+    result."""
     buf, _, _ = gen.gen_c4(3000, seed=11)
     b = buf.tobytes()
     K = (len(b) + R - 1) // R
@@ -216,4 +278,4 @@ def test_model_adjacent_wrong_guesses_any_chase_order():
                 bad[k] = k * R + int(rng.integers(0, R))
         if trial % 4 == 1:  # a wrong guess pointing into the next region
             bad[a + 1] = (a + 2) * R + 17
-        check(b, inject=bad, order_seed=trial)
+        check(b, inject=bad, order_seed=trial, block=(5, 8, 256)[trial % 3])
