@@ -282,7 +282,20 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
 template <int NCH, uint32_t GM, int WK, bool STAGED = false>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own, uint64_t* pkt_st);
+                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T);
+
+// Dynamic LDS of a lockstep launch: the windows (or spans), then the dispatch tables.
+__host__ __device__ constexpr size_t with_tables(size_t bytes, int wk) {
+    return wk == 1 ? ((bytes + 15) & ~(size_t)15) + sizeof(DispatchLds) : bytes;
+}
+template <int WK>
+__device__ __forceinline__ const DispatchLds* tables(uint8_t* lds, size_t at, uint32_t t, uint32_t nt) {
+    if constexpr (WK != 1) return nullptr;
+    DispatchLds* T = reinterpret_cast<DispatchLds*>(lds + ((at + 15) & ~(size_t)15));
+    dispatch_init(T, t, nt);
+    __syncthreads();
+    return T;
+}
 
 // One block = 256 packets, one lane per packet.  (A persistent grid of k blocks per CU striding
 // over the tiles, each lane's loads of its next packet in flight while it parsed the current one,
@@ -298,6 +311,7 @@ void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
     PKT_STAMP(0);
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
     const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
     const bool act = base + threadIdx.x < p.n;
     u32x4 chunk[NCH];
@@ -341,17 +355,17 @@ void parse_kernel(KParams p) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         PKT_STAMP(1);
-        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act, pkt_st);
+        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act, pkt_st, T);
         return;
     }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act, pkt_st);
+    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act, pkt_st, T);
 }
 
 template <int NCH, uint32_t GM, int WK, bool STAGED>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own, uint64_t* pkt_st) {
+                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T) {
     (void)pkt_st;
     const uint32_t t = threadIdx.x;
     const uint32_t i_own = base + t;
@@ -422,12 +436,16 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     // each lane walks and emits its own packet (no barrier: own LDS only)
     __builtin_amdgcn_wave_barrier();
     WalkResult r;
-    walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r);
+    walk<WK>(pv_own, entry_state(p.entry), active_own && !fast, push, r, T);
     if constexpr (NCH >= 4) {
         if (fast) fast_result(r, fv);
     }
     PKT_STAMP(2);
     if (active_own) {
+        // (the column bases stay in SGPRs from the kernel start: C4 all columns keeps 106 SGPRs and
+        // spills 48 to VGPR lanes, ~96 lane instructions per wave; loading them after the walk
+        // through an opaque copy of the argument pointer made every column access a flat access:
+        // 6x slower, profiles/ab/r03j_late_column_pointers.txt)
         emit_chain<GM>(out, i_own, len_own, r);
         emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
     }
@@ -475,6 +493,7 @@ template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x;
+    const DispatchLds* T = tables<WK>(lds, span_region(NCH), lane, kSpanBlock);
     const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
     const bool active = i < p.n;
     uint64_t off = 0;
@@ -527,7 +546,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     const uint64_t ns = p.n_slot_stride;
     auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) { push_slot<GM>(out, ns, slot, i, ty, o); };
     WalkResult r;
-    walk<WK>(pv, entry_state(p.entry), active, push, r);
+    walk<WK>(pv, entry_state(p.entry), active, push, r, T);
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
@@ -593,6 +612,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_wav
 void parse_pipe_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
     const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
     const uint32_t ntiles = (p.n + 63u) / 64u;
     const uint32_t W = gridDim.x * (uint32_t)kWavesPerBlock;
@@ -618,7 +638,7 @@ void parse_pipe_kernel(KParams p) {
         tile_range<NCH>(p, tile + 2 * W, wl, off2, len2);
         // walk and emit this tile from LDS
         const uint32_t base = tile * 64u - wave0;  // parse_tile's lane index = base + threadIdx.x
-        parse_tile<NCH, GM, WK, true>(p, lds, base, none, off, len, tile * 64u + wl < p.n, pkt_st);
+        parse_tile<NCH, GM, WK, true>(p, lds, base, none, off, len, tile * 64u + wl < p.n, pkt_st, T);
         off = off1;
         len = len1;
         off1 = off2;
@@ -640,18 +660,19 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
         (void)hipGetDevice(&dev);
         (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
         const uint32_t per_cu = std::max<uint32_t>(
-            1u, std::min<uint32_t>((uint32_t)((160u * 1024u) / window_lds(NCH)),
+            1u, std::min<uint32_t>((uint32_t)((160u * 1024u) / with_tables(window_lds(NCH), WK)),
                                    (uint32_t)(4 * pipe_waves_per_eu(NCH, GM) / kWavesPerBlock)));
         const uint32_t tiles = (kp.n + 63u) / 64u;
         const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus * per_cu, (tiles + kWavesPerBlock - 1) / kWavesPerBlock));
-        hipLaunchKernelGGL((parse_pipe_kernel<NCH, GM, WK>), dim3(blocks), dim3(kBlock), window_lds(NCH), s, kp);
+        hipLaunchKernelGGL((parse_pipe_kernel<NCH, GM, WK>), dim3(blocks), dim3(kBlock),
+                           with_tables(window_lds(NCH), WK), s, kp);
         return hipGetLastError();
     }
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
-                           dim3(kSpanBlock), span_region(NCH), s, kp);
+                           dim3(kSpanBlock), with_tables(span_region(NCH), WK), s, kp);
     } else {
-        const size_t lds = window_lds(NCH);
+        const size_t lds = with_tables(window_lds(NCH), WK);
         hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }

@@ -90,6 +90,42 @@ __device__ __forceinline__ uint32_t gre_next(uint32_t p) {
     return s;
 }
 
+// Dispatch tables of the lockstep step, in LDS (built per block by dispatch_init, 576 bytes):
+//   et[h(v)]  for the 16-bit dispatch values of parse_ethernet / parse_vlan (types.rs:51-75) and
+//             parse_gre (fast.rs:147-153): key v << 10 | GRE next state << 5 | EtherType next state,
+//             h(v) = (v * 355 >> 12) & 15 — a perfect hash of the 7 values that dispatch anywhere
+//             (8100 0806 0800 86DD 8847 88BE 22EB); every other value misses its slot's key -> accept
+//   ip[p]     the IPv4 (low 5 bits) and IPv6 (next 5 bits) next state of protocol byte p
+//             (fast.rs:87-95, 102-110; Q6)
+// One LDS read each instead of the compare chains (which the compiler turned into divergent
+// branches, all taken by a mixed wave).
+struct DispatchLds {
+    uint32_t et[16];
+    uint16_t ip[256];
+};
+constexpr uint32_t kDispatchKeys[7] = {0x8100u, 0x0806u, 0x0800u, 0x86DDu, 0x8847u, 0x88BEu, 0x22EBu};
+__host__ __device__ constexpr uint32_t et_hash(uint32_t v) { return ((v * 355u) >> 12) & 15u; }
+constexpr bool et_hash_perfect() {
+    for (int a = 0; a < 7; a++)
+        for (int b = a + 1; b < 7; b++)
+            if (et_hash(kDispatchKeys[a]) == et_hash(kDispatchKeys[b])) return false;
+    return true;
+}
+static_assert(et_hash_perfect(), "the dispatch hash must separate the 7 dispatching values");
+
+// Thread t of a block of nt threads builds its share of the tables (the caller then syncs).
+__device__ __forceinline__ void dispatch_init(DispatchLds* T, uint32_t t, uint32_t nt) {
+    for (uint32_t p = t; p < 256u; p += nt) T->ip[p] = (uint16_t)(ipproto_next(p, false) | (ipproto_next(p, true) << 5));
+    for (uint32_t h = t; h < 16u; h += nt) {
+        uint32_t e = (0x1FFFFu << 10) | ((uint32_t)S_ACCEPT << 5) | S_ACCEPT;  // a key no 16-bit value has
+#pragma unroll
+        for (int k = 0; k < 7; k++)
+            if (et_hash(kDispatchKeys[k]) == h)
+                e = (kDispatchKeys[k] << 10) | (gre_next(kDispatchKeys[k]) << 5) | etype_next(kDispatchKeys[k]);
+        T->et[h] = e;
+    }
+}
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // A lane's view of its packet: LDS window + global fallback.
@@ -339,7 +375,8 @@ constexpr uint64_t kDw0 = pack6(kDwLo, 0), kDw1 = pack6(kDwHi, 10);
 __device__ __forceinline__ uint32_t tab6(uint64_t lo, uint64_t hi, uint32_t st) {
     const bool h = st >= 10u;
     const uint64_t t = h ? hi : lo;
-    return (uint32_t)(t >> (6u * (h ? st - 10u : st))) & 63u;
+    // 24-bit multiply (full rate; a 32-bit v_mul_lo_u32 issues at quarter rate)
+    return (uint32_t)(t >> __umul24(6u, h ? st - 10u : st)) & 63u;
 }
 
 // One lockstep iteration for every live lane: the header of the lane's state is checked, read and
@@ -369,13 +406,21 @@ __device__ __forceinline__ void lrec_opt(LockLane& L, uint32_t t, uint32_t off, 
 // slot stores and the rare GRE-option / ERSPAN-platform records branch), so the compiler keeps
 // one copy of the lane state instead of re-materialising it at every divergent merge.
 template <class Push>
-__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push, bool live) {
+__device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Push& push, bool live,
+                                      const DispatchLds* T) {
     const uint32_t st = L.st, o = L.o;
     const uint32_t sz = tab6(kSz0, kSz1, st);
     const uint32_t hw = D >> 16;
-    const uint32_t et_next = etype_next(hw);
+    // table dispatch: the 16-bit value (EtherType, or GRE's protocol in the dword's low half) and
+    // the IP protocol byte, one LDS read each
+    const uint32_t k16 = st == S_GRE ? (D & 0xFFFFu) : hw;
+    const uint32_t te = T->et[et_hash(k16)];
+    const bool hit = (te >> 10) == k16;
+    const uint32_t et_next = hit ? (te & 31u) : (uint32_t)S_ACCEPT;
+    const uint32_t gr_next = hit ? ((te >> 5) & 31u) : (uint32_t)S_ACCEPT;
     const bool v6 = st == S_IPV6;
-    const uint32_t ip_next = ipproto_next(v6 ? (D >> 8) & 0xFFu : hw & 0xFFu, v6);
+    const uint32_t ti = T->ip[v6 ? (D >> 8) & 0xFFu : hw & 0xFFu];
+    const uint32_t ip_next = v6 ? (uint32_t)(ti >> 5) : (uint32_t)(ti & 31u);
     uint32_t nx = S_ACCEPT;  // SNAP, ARP, ICMP, TCP
     nx = (st == S_PARSE) ? (hw < 1500u ? S_DOT3 : S_ETHER) : nx;
     nx = (st == S_DOT3) ? S_LLC : nx;
@@ -384,7 +429,7 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
     nx = (st == S_MPLS) ? (((D >> 8) & 1u) ? S_MPLS_BOS : S_MPLS) : nx;
     nx = (st == S_MPLS_BOS) ? ((D >> 28) == 4u ? S_IPV4 : ((D >> 28) == 6u ? S_IPV6 : S_ETHER)) : nx;
     nx = (st == S_IPV4 || st == S_IPV6) ? ip_next : nx;
-    nx = (st == S_GRE) ? gre_next(D & 0xFFFFu) : nx;
+    nx = (st == S_GRE) ? gr_next : nx;
     nx = (st == S_ERSPAN2 || st == S_ERSPAN3 || st == S_VXLAN) ? S_ETHER : nx;
     nx = (st == S_UDP) ? (hw == 4789u ? S_VXLAN : S_ACCEPT) : nx;
     // the reference's panics in its order: iteration bound (walk), `&arr[0..X::size()]`, depth,
@@ -462,7 +507,7 @@ __device__ __forceinline__ void lstep(LockLane& L, uint32_t len, uint32_t D, Pus
 // indexed windows to hold every header the 22 templates carry, parse_kernel.)
 template <int WK, class Push>
 __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active, Push&& push,
-                                     WalkResult& out) {
+                                     WalkResult& out, const DispatchLds* T = nullptr) {
     if constexpr (WK == 1) {
         LockLane L{state, 0, 0, 0, PKT_OK, 0, 0, active, {-1, -1, -1, -1, -1, -1}};
         if (state == S_PARSE) {
@@ -491,7 +536,7 @@ __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active
             if (__ballot(far)) {
                 if (far) D = pv.le(b, 4);
             }
-            lstep(L, pv.len, bswap32(D), push, live);
+            lstep(L, pv.len, bswap32(D), push, live, T);
         }
         out.status = L.status;
         out.n = L.n;
