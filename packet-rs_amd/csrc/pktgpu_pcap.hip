@@ -332,6 +332,9 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     const uint64_t entry = k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k);
     uint64_t exit;
     uint32_t cnt, err, rec;
+    // (w = readfirstlane(t / 64), which lets the compiler see k as uniform and turn the walk into a
+    // scalar loop — VALU per hop 20 -> 5, SALU 14 -> 17 — measured slower: 111 vs 102 us per call,
+    // profiles/ab/r03n_pcap_uniform_wave.txt)
     // (the walk reading each incl_len by scalar-unit loads from L2 instead of LDS halves the VALU
     // instructions, 736 -> 374 per wave, but each hop then waits ~3x longer: 80 vs 63 us per call,
     // profiles/ab/r03i_pcap_uniform_walk.txt)
@@ -618,6 +621,9 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         vm_drain();
         st_agent(&my->i_meta, ((uint64_t)S.epoch << 8) | kPublished | err_all);
         if (blk == nb - 1) {
+            // every block has taken its ticket by now (this one took the last): the next call's
+            // tickets start at 0 without a memset launch on the call's critical path (4.7 us)
+            if (ticket) st_agent(S.ticket, 0u);
             __hip_atomic_store(&S.host[kHostTotal], c_before + total.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err_all ? 1 : 0), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
@@ -750,7 +756,6 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
     if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
     e = hipGetLastError();
-    if (e == hipSuccess) e = hipMemsetAsync(S.ticket, 0, 4, s);  // the next call's tickets start at 0
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "pcap index");
     if (!pc.ctl[kHostMagic]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");

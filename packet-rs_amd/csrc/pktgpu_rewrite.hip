@@ -132,6 +132,24 @@ __device__ __forceinline__ int32_t find_lds(const ChainLds& L, const BatchRef& b
     return -1;
 }
 
+// The same search over the chain's first 4 slots held in registers (chain_load's, branch-free
+// selects: no loop, no LDS read); only a chain of more than 4 headers without a match among them
+// goes on to find_lds.  (extract 19 getters 61.7 -> 57.8 us, set_fields + checksum 49.8 -> 40.4 us
+// together with set_in_window's dword write-back, profiles/ab/r03p_rewrite_kernels.txt)
+__device__ __forceinline__ int32_t find_pre(const ChainPre& c, const ChainLds& L, const BatchRef& b, uint64_t i,
+                                            uint32_t t, uint32_t nh, uint32_t type, uint32_t occ) {
+    int32_t r = -1;
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+        const bool m = j < nh && c.ty[j] == type;
+        r = (m && cnt == occ && r < 0) ? (int32_t)c.of[j] : r;
+        cnt += m ? 1u : 0u;
+    }
+    if (r < 0 && nh > 4) r = find_lds(L, b, i, t, nh, type, occ);
+    return r;
+}
+
 struct XSpec {
     pkt_field_spec_t f;
     uint64_t* values;
@@ -203,7 +221,7 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
     for (uint32_t s = 0; s < p.nspec; s++) {  // uniform
         const pkt_field_spec_t sp = S[s].f;
         if (sp.hdr_type != last_ty || sp.occurrence != last_occ) {  // consecutive specs of one header: one search
-            ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
+            ho = find_pre(cp, L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
             last_ty = sp.hdr_type;
             last_occ = sp.occurrence;
         }
@@ -343,9 +361,13 @@ __device__ __forceinline__ void load_src_chunk(const BatchRef& b, uint64_t last1
     }
 }
 
+constexpr uint32_t kTvMapChunks = 2048;  // chunks per wave the start map covers (32 KiB of output)
+
 __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     const uint32_t lane = threadIdx.x & 63u;
-    const uint64_t base = ((uint64_t)blockIdx.x * kRwBlock + (threadIdx.x & ~63u));  // wave's first packet
+    // wave-uniform values through readfirstlane (the compiler cannot tell threadIdx.x & ~63 is)
+    const uint64_t base = ((uint64_t)blockIdx.x * kRwBlock +
+                           __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u));  // wave's first packet
     const uint64_t i = base + lane;
     // ---- per-lane metadata of packet i (coalesced column reads)
     uint64_t src = 0, dst = 0;
@@ -379,10 +401,13 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     // packet's chunks are consecutive, packets in lane order), lane j copying chunks j, j+64, ...:
     // a wave-instruction writes 64 consecutive chunks whatever the packet lengths (records of a
     // capture lie back to back, so mostly 1 KiB of contiguous destination)
-    const uint32_t w = threadIdx.x >> 6;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     __shared__ uint32_t s_pre[kRwBlock / 64][65];
     __shared__ uint64_t s_src[kRwBlock / 64][64], s_dst[kRwBlock / 64][64];
     __shared__ uint32_t s_len[kRwBlock / 64][64];
+    __shared__ uint64_t s_map[kRwBlock / 64][kTvMapChunks / 64];
+    __shared__ uint64_t s_csrc[kRwBlock / 64][64], s_cdst[kRwBlock / 64][64];
+    __shared__ uint32_t s_clen[kRwBlock / 64][64], s_cpre[kRwBlock / 64][64];
     const bool flat = ok && ident && len > 0;
     const uint32_t ch = flat ? (uint32_t)(((dst & 15) + len + 15) >> 4) : 0u;
     uint32_t incl = ch;  // inclusive scan over the wave
@@ -401,6 +426,35 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    // Chunk -> packet without a search: bit g of the wave's start map is set iff a packet's first
+    // chunk is g, and the flat packets' (src, dst, len, pre) are stored compacted by rank, so chunk
+    // g = 64 r + lane belongs to rank (starts before round r) + (starts at or below g within the
+    // round's 64-bit word) - 1: one broadcast LDS read and a v_mbcnt per round instead of the
+    // per-lane chain of dependent LDS compares (C2 30.8 -> 28.3 us; C4 unchanged,
+    // profiles/ab/r03p_rewrite_kernels.txt).  Waves of more than kTvMapChunks chunks keep the search.
+    const bool use_map = total <= kTvMapChunks;  // uniform
+    if (use_map) {
+        if (lane < kTvMapChunks / 64) s_map[w][lane] = 0;
+        const uint64_t fm = __ballot(ch != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
+        if (ch) {
+            s_csrc[w][rank] = src;
+            s_cdst[w][rank] = dst;
+            s_clen[w][rank] = len;
+            s_cpre[w][rank] = incl - ch;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (ch) {
+            const uint32_t g0 = incl - ch;
+            atomicOr(reinterpret_cast<uint32_t*>(s_map[w]) + (g0 >> 5), 1u << (g0 & 31u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    uint32_t run = 0;  // starts in the rounds before the one being located (uniform)
     // A wave whose 64 outputs lie back to back in the destination (a fixed-stride slab of whole
     // slots, or packed outputs) stores its whole chunks non-temporally: C2 33.7 -> 30.8 us, C4
     // packed 119 -> 102 us; with gaps between the outputs (a pcap's record headers left untouched)
@@ -416,10 +470,19 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     // VGPRs halve the resident waves, profiles/ab/r02tv_to_vec_unroll.txt.)
     uint32_t k = 0;
     auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4]) {
-        while (s_pre[w][k + 1] <= g) k++;  // packets with no chunks are skipped (pre[64] = total > g)
-        const uint64_t s = s_src[w][k], d = s_dst[w][k];
-        const uint32_t L = s_len[w][k];
-        ca = (d & ~(uint64_t)15) + 16u * (g - s_pre[w][k]);  // destination chunk
+        uint64_t s, d;
+        uint32_t L, pre;
+        if (use_map) {  // rounds are located in order, each once
+            const uint64_t word = s_map[w][g >> 6];
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(word >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)word, 0u));
+            const uint32_t r = run + below + (uint32_t)((word >> lane) & 1u) - 1u;
+            run += (uint32_t)__builtin_popcountll(word);
+            s = s_csrc[w][r], d = s_cdst[w][r], L = s_clen[w][r], pre = s_cpre[w][r];
+        } else {
+            while (s_pre[w][k + 1] <= g) k++;  // packets with no chunks are skipped (pre[64] = total > g)
+            s = s_src[w][k], d = s_dst[w][k], L = s_len[w][k], pre = s_pre[w][k];
+        }
+        ca = (d & ~(uint64_t)15) + 16u * (g - pre);  // destination chunk
         load_src_chunk(p.b, last16, s, d, ca, o);
         lo = ca > d ? ca : d;
         hi = ca + 16 < d + L ? ca + 16 : d + L;
@@ -506,8 +569,20 @@ __device__ __forceinline__ void set_in_window(uint32_t* w, uint32_t x, uint32_t 
            ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(d3, d2, sh)) << 32) |
                __builtin_bswap32(__builtin_amdgcn_alignbyte(d4, d3, sh))};
     put_bits(W, lsb - 8 * b0, msb - 8 * b0, msb - lsb + 1, v, 0);
-    uint8_t* h = reinterpret_cast<uint8_t*>(w) + x;
-    for (uint32_t j = 0; j < nb; j++) h[j] = (uint8_t)((j < 8 ? W.hi >> (56 - 8 * j) : W.lo >> (120 - 8 * j)) & 0xFFu);
+    // back as the aligned dwords holding the field's bytes (at most 3: sh + nb <= 12), rebuilt from
+    // W's little-endian dwords e_j (bytes x + 4j ..) by a funnel shift; the bytes around the field
+    // are rewritten with the values just read (the lane's own window)
+    const uint32_t e0 = __builtin_bswap32((uint32_t)(W.hi >> 32)), e1 = __builtin_bswap32((uint32_t)W.hi);
+    const uint32_t e2 = __builtin_bswap32((uint32_t)(W.lo >> 32));
+    const uint32_t em = sh ? d0 << (32 - 8 * sh) : 0u;  // top sh bytes = d0's bytes before x
+    const uint32_t s4 = 4 - sh;
+    const uint32_t n0 = sh ? __builtin_amdgcn_alignbyte(e0, em, s4) : e0;
+    const uint32_t n1 = sh ? __builtin_amdgcn_alignbyte(e1, e0, s4) : e1;
+    const uint32_t n2 = sh ? __builtin_amdgcn_alignbyte(e2, e1, s4) : e2;
+    const uint32_t jl = (sh + nb - 1) >> 2;
+    w[k] = n0;
+    if (jl >= 1) w[k + 1] = n1;
+    if (jl >= 2) w[k + 2] = n2;
 }
 
 template <int NCH>
@@ -563,14 +638,14 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     bool inwin = act;
     for (uint32_t s = 0; s < p.nspec && inwin; s++) {
         const pkt_field_spec_t sp = S[s].f;
-        const int32_t ho = act ? find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
+        const int32_t ho = act ? find_pre(cp, L, p.b, i, t, nh, sp.hdr_type, sp.occurrence) : -1;
         if (ho >= 0 && (sp.end - sp.start >= 64 || shift + (uint32_t)ho + (sp.end >> 3) + 1 > 16u * NCH)) inwin = false;
     }
     uint32_t dirty = 0;  // window chunks holding a set byte
     // one setter (specs in order: overlapping ones act as sequential setters)
     auto apply = [&](uint32_t s, uint64_t v0) {
         const pkt_field_spec_t sp = S[s].f;
-        const int32_t ho = find_lds(L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
+        const int32_t ho = find_pre(cp, L, p.b, i, t, nh, sp.hdr_type, sp.occurrence);
         if (ho < 0) return;
         const uint32_t lsb = sp.start, msb = sp.end;
         if (inwin) {
@@ -625,7 +700,7 @@ __global__ __launch_bounds__(kRwBlock) void set_fields_kernel(SParams p) {
     // the setters: header dwords inside the window from LDS, past it from global memory (bytes only
     // this lane wrote); the two checksum bytes into LDS (dirty) or global memory likewise.
     if (p.csum_occ >= 0 && act) {
-        const int32_t ho = find_lds(L, p.b, i, t, nh, PKT_HDR_IPV4, (uint32_t)p.csum_occ);
+        const int32_t ho = find_pre(cp, L, p.b, i, t, nh, PKT_HDR_IPV4, (uint32_t)p.csum_occ);
         if (ho >= 0) {
             const uint32_t x = shift + (uint32_t)ho, x0 = x & ~3u, sh = x & 3u;
             const uint64_t a0 = off & ~(uint64_t)15;  // window byte q <-> slab byte a0 + q
