@@ -703,7 +703,8 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
                      "bytes_into_root": into_root,
                      "GB/s_into_root": round(into_root / gather_s / 1e9, 2) if into_root else None,
                      "bytes_root_local": moved[0],
-                     "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI)",
+                     "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI); the root's own shard "
+                                "by hipMemcpyAsync on the root stream",
                      "timing": "wall clock around each blocking call (+ synchronize), median of 5; "
                                "gather = (parse + gather) - parse"}
     return rec

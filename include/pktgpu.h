@@ -490,7 +490,8 @@ int pkt_mgpu_parse_steps(pkt_mgpu_t *mg, const pkt_batch_t *batches, int steps, 
                          void *const *shard_out, int streams);
 /* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
  * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.
- * Grouped ncclSend/ncclRecv (the root's own block is a send to itself). */
+ * Grouped ncclSend/ncclRecv from the other devices; the root's own block is a device copy on the
+ * root's stream (an RCCL send to itself moved ~1 TB/s, the copy ~2 TB/s). */
 int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uint64_t *bytes,
                     void *recv, uint64_t recv_len, const uint64_t *recv_off);
 /* pkt_mgpu_parse, then the gather of every shard's packed tuple buffer into `recv` on the root
@@ -501,7 +502,7 @@ int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uin
  * tuples land as ONE packed output of sum(n) packets instead (recv = pkt_out_packed(col_mask,
  * sum n) bytes, shards in order: what pkt_parse_batch over the whole batch would write); the
  * gather then sends each column (each slot row) of a shard as its own message, and root_views[0]
- * receives that single view. */
+ * receives that single view.  The root's own pieces are device copies, as in pkt_mgpu_gather. */
 int pkt_mgpu_parse_gather(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
                           void *const *shard_out, int root, void *recv, uint64_t recv_len,
                           int merge, pkt_out_t *root_views);

@@ -40,9 +40,6 @@ namespace {
 __constant__ uint8_t kHdrSize[PKT_HDR_COUNT] = {0, 14, 4, 20, 40, 4, 20, 8, 28, 8, 14, 3, 5, 4, 4, 4, 4, 8, 12, 8, 35, 4};
 
 constexpr uint32_t kRwBlock = 256;
-#ifndef PKTGPU_X_NT
-#define PKTGPU_X_NT 1  // non-temporal getter output columns: 19 getters 65.5 -> 62.4 us (profiles/ab/r02xnt_extract_nt.txt)
-#endif
 constexpr int kMaxSpecs = 32;  // specs per launch (extract / set_fields)
 static_assert(kRwBlock >= (uint32_t)kMaxSpecs, "one thread copies each spec into the LDS spec table");
 
@@ -247,13 +244,9 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
             if (w2 != 0 && w2 < 64) val &= (1ull << w2) - 1;
             v = val;
         }
-#if PKTGPU_X_NT
+        // non-temporal getter output columns: 19 getters 65.5 -> 62.4 us (profiles/ab/r02xnt_extract_nt.txt)
         __builtin_nontemporal_store(v, S[s].values + i);
         if (S[s].found) __builtin_nontemporal_store((uint8_t)(ho >= 0 ? 1 : 0), S[s].found + i);
-#else
-        S[s].values[i] = v;
-        if (S[s].found) S[s].found[i] = ho >= 0 ? 1 : 0;
-#endif
     }
 }
 
