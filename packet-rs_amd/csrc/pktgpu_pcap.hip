@@ -209,31 +209,38 @@ __device__ __forceinline__ void stage(uint4* l4, const uint8_t* buf, uint64_t ba
 // Walk the records from `entry` while they start inside the region [base, base + kRegion) and
 // 16 header bytes remain: pkt_pcap_index's loop restated per region.  Record i's offset in the
 // region is kept by lane i in `rec` (a select per record, no branch, no LDS write); records 64..
-// (regions of short records) go to `list` from lane 0.  The position lives in an SGPR
-// (readfirstlane of each LDS read), so the loop's bounds checks are SALU compares and its branches
-// uniform, with 32-bit offsets from lbase while the file's end is < 4 GiB past it; otherwise the
-// 64-bit vector form.
+// (regions of short records) go to `list` from lane 0.  32-bit offsets from the region base while
+// the file's end is < 4 GiB past the staged bytes, otherwise the 64-bit form.  The position stays a
+// vector value: a scalar walk (readfirstlane of each incl_len, SALU bounds checks) is slower, its
+// per-hop chain VALU -> SGPR -> SALU -> VALU longer (111 vs 99 us per call), and the lean vector
+// loop (one bound, no masks) beats the round-2 form 99 vs 102 us (profiles/ab/r03t_pcap_walk.txt).
 __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_t* list, uint64_t base,
                                      uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt, uint32_t& err,
                                      uint32_t& rec) {
     if (len - lbase <= 0xFFFFFFF0ull && entry - lbase <= 0xFFFFFFF0ull) {
         const uint32_t lane = lane_id();
-        const uint32_t rb = (uint32_t)(base - lbase), rend = rb + kRegion, rlen = (uint32_t)(len - lbase);
-        uint32_t p = __builtin_amdgcn_readfirstlane((uint32_t)(entry - lbase));
+        // q = the record's start relative to the region base (base < len: room >= 1); the walk goes
+        // on while q < kRegion and 16 header bytes remain (q <= room - 16); incl_len = bytes
+        // q + 8 .. q + 11 (v_alignbyte takes the shift's low two bits: no mask)
+        const uint32_t rb = (uint32_t)(base - lbase), room = (uint32_t)(len - lbase) - rb;
+        const uint32_t lim = room >= 16 ? (room - 15 < kRegion ? room - 15 : kRegion) : 0u;
+        const uint32_t* lr = lw + (rb >> 2);
+        uint32_t q = entry >= base ? (uint32_t)(entry - base) : kRegion;  // (entry >= base always)
         uint32_t c = 0, e = 0, rv = 0;
-        while (p < rend && p + 16 <= rlen) {
-            const uint32_t incl = __builtin_amdgcn_readfirstlane(ld32(lw, p + 8));
-            if (incl > rlen - p - 16) {  // pkt_pcap_index: record runs past the end
+        while (q < lim) {
+            const uint32_t k2 = (q >> 2) + 2;
+            const uint32_t incl = __builtin_amdgcn_alignbyte(lr[k2 + 1], lr[k2], q);
+            if (incl > room - 16 - q) {  // pkt_pcap_index: record runs past the end
                 e = 1;
-                p = rlen;
+                q = room;
                 break;
             }
-            rv = lane == c ? p - rb : rv;
-            if (c >= 64u && c < kMaxRec && lane == 0) list[c] = (uint16_t)(p - rb);
+            rv = lane == c ? q : rv;
+            if (c >= 64u && c < kMaxRec && lane == 0) list[c] = (uint16_t)q;
             c++;
-            p += 16 + incl;
+            q += 16 + incl;
         }
-        exit = lbase + p;
+        exit = base + q;
         cnt = c;
         err = e;
         rec = rv;
