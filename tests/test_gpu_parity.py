@@ -447,6 +447,47 @@ def test_to_vec_c4_dst_layouts_vs_oracle(P, shift):
     assert (o[mask] == 0xEE).all()
 
 
+def test_to_vec_long_packets_both_chunk_maps_vs_oracle(P):
+    """Waves whose outputs exceed the kernel's per-wave start map (> 2048 16-byte chunks: 64
+    records of ~1.4 KB) next to waves of short records (the map path), in a pcap-like layout with
+    16-byte gaps, plus truncated records: every to_vec equals the oracle's slow::parse(..).to_vec()
+    and no gap byte of the destination changes (tests/lib.rs:790-802 round trip)."""
+    n = 512
+    pkts = []
+    for i in range(n):
+        big = (i // 64) % 2 == 0
+        pay = bytes((i * 7 + j) & 0xFF for j in range(1400 - (i % 9) if big else i % 50))
+        pkts.append(gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                          "1.1.1.1", "2.2.2.2", 0, 64, 0, 0, [], 1000 + i, 2000, False,
+                                          pay).to_vec())
+    for i in range(3, n, 97):
+        pkts[i] = pkts[i][:20]  # truncated: not written, out_len 0
+    lens = np.array([len(x) for x in pkts], np.uint32)
+    offs = np.concatenate([[16], 16 + np.cumsum(lens.astype(np.uint64) + np.uint64(16))[:-1]]).astype(np.uint64)
+    total = int(offs[-1]) + int(lens[-1]) + 16
+    buf = bytearray(total)
+    for i, x in enumerate(pkts):
+        buf[int(offs[i]):int(offs[i]) + len(x)] = x
+    slab = np.frombuffer(bytes(buf), np.uint8)
+    ds, do, dl = dev(slab), dev(offs), dev(lens)
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst = torch.full((total,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst)
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    mask = np.ones(total, bool)
+    for i, x in enumerate(pkts):
+        try:
+            want = oracle.slow_parse_to_vec(x)
+        except ValueError:
+            assert ln[i] == 0, i
+            continue
+        assert ln[i] == len(want), i
+        assert o[int(offs[i]):int(offs[i]) + len(want)].tobytes() == want, i
+        mask[int(offs[i]):int(offs[i]) + len(want)] = False
+    assert (o[mask] == 0xEE).all()
+
+
 # ------------------------------------------------------------------ mixed inputs
 def test_mixed_inputs_bit_exact(P):
     """The reference pcap, a C4 replay, C3/C2 slabs and random/truncated records under three
