@@ -223,17 +223,32 @@ __global__ __launch_bounds__(kRwBlock) void extract_kernel(XParams p) {
             last_occ = sp.occurrence;
         }
         uint64_t v = 0;
+        const uint32_t start = sp.start, end = sp.end, wd = end - start + 1;
+        // bits [s2..end] hold the low 64 bits of the field; bit_range's release-build shifts
+        // then keep the low (w mod 64, or 64) of them (headers.rs:262, Q8)
+        const uint32_t s2 = wd > 64 ? end - 63 : start;
+        const uint32_t b0 = s2 >> 3, b1 = end >> 3;  // <= 9 bytes
+        const uint32_t rel = ho >= 0 ? (uint32_t)ho + b0 : 0u;
+        const uint32_t nb = b1 - b0 + 1;
+        // When every lane of the wave that has the header holds bytes rel .. rel + 11 in its window
+        // (the common case), three straight LDS dword reads; else le() per lane (window or memory):
+        // 19 getters 59.3 -> 54.9 us (profiles/ab/r03z_extract_uniform_window.txt).
+        uint32_t x0, x1, x8;
+        if (!__ballot(ho >= 0 && rel + 12u > pv.win_end)) {  // uniform
+            const uint32_t wb = rel + pv.shift, k = wb >> 2, sh = wb & 3;
+            const uint32_t d0 = w[k], d1 = w[k + 1], d2 = w[k + 2];
+            x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            x8 = d2 >> (8u * sh);
+        } else {
+            x0 = ho >= 0 ? pv.le(rel, 4) : 0u;
+            x1 = ho >= 0 ? pv.le(rel + 4, 4) : 0u;
+            x8 = (ho >= 0 && nb == 9) ? pv.le(rel + 8, 1) : 0u;
+        }
         if (ho >= 0) {
-            const uint32_t start = sp.start, end = sp.end, wd = end - start + 1;
-            // bits [s2..end] hold the low 64 bits of the field; bit_range's release-build shifts
-            // then keep the low (w mod 64, or 64) of them (headers.rs:262, Q8)
-            const uint32_t s2 = wd > 64 ? end - 63 : start;
-            const uint32_t b0 = s2 >> 3, b1 = end >> 3;  // <= 9 bytes
-            const uint32_t rel = (uint32_t)ho + b0;
             // bytes b0.. as big-endian: 8 in hi, the 9th (if any) in the top byte of x2
-            const uint64_t hi = ((uint64_t)__builtin_bswap32(pv.le(rel, 4)) << 32) | __builtin_bswap32(pv.le(rel + 4, 4));
-            const uint32_t nb = b1 - b0 + 1;
-            const uint32_t ninth = nb == 9 ? pv.le(rel + 8, 1) & 0xFFu : 0u;
+            const uint64_t hi = ((uint64_t)__builtin_bswap32(x0) << 32) | __builtin_bswap32(x1);
+            const uint32_t ninth = nb == 9 ? x8 & 0xFFu : 0u;
             // value = bytes b0..b1 as a big-endian integer, shifted right by the trailing bits
             const uint32_t r = 7 - (end & 7);
             uint64_t acc, top;

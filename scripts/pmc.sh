@@ -1,6 +1,7 @@
 #!/bin/bash
-# PMC passes (one counter group per rocprofv3 run, kernel-trace only) over a kbench variant, or
-# over the device pcap indexer (config "pcap": scripts/pcap_index_bench.py).
+# PMC passes (one counter group per rocprofv3 run, kernel-trace only) over a kbench variant, over
+# the device pcap indexer (config "pcap": scripts/pcap_index_bench.py), or over secondary_bench
+# workloads (config "secondary", variant = its --only list).
 # usage: scripts/pmc.sh TAG "variant" [config] [extra kbench args]
 set -u
 TAG=$1; VAR=$2; CFG=${3:-c2}; EXTRA=${4:-}
@@ -8,6 +9,7 @@ OUT=gpurun_out/$TAG; mkdir -p $OUT
 export TMPDIR=/tmp
 rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 if [ "$CFG" = pcap ]; then PROG="scripts/pcap_index_bench.py --reps 5 --no-check"
+elif [ "$CFG" = secondary ]; then PROG="scripts/secondary_bench.py --only $VAR --cpu-budget 0.02 --iters 5"
 else PROG="scripts/kbench.py --config $CFG --variants $VAR --rounds 1 --iters 12 $EXTRA"; fi
 run() {  # name, counters...
   local name=$1; shift
