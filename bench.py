@@ -17,7 +17,7 @@ exchange (fast::parse is a pure function of one packet, reference src/parser/fas
 torch.distributed.run rank 0 is that process and the other ranks wait at a CPU (gloo) barrier
 without touching a GPU.  The "c5" record times the C5 config through pkt_mgpu_parse_gather: 2^24
 packets in contiguous shards, parse and RCCL gather of the used tuple bytes to device 0 timed
-separately.  --per-rank keeps the one-process-per-GPU torch.distributed form.
+separately.
 At N = 1 the line also carries the host-memory rate ("host": pinned zero-copy pkt_parse_host) and
 the capture path ("pcap": capture in HBM -> pkt_pcap_index_device -> parse, one step).
 
@@ -26,8 +26,6 @@ Prints ONE JSON line (see DESIGN.md "Measurement" for every field).
 import argparse
 import json
 import os
-import socket
-import subprocess
 import sys
 import time
 
@@ -56,7 +54,6 @@ def parse_args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 record")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every core this process may use")
-    ap.add_argument("--backend", default="nccl", help="torch.distributed backend (nccl = RCCL)")
     ap.add_argument("--fastpath", type=int, default=int(os.environ.get("PKTGPU_FASTPATH", "1")),
                     help="register fast path for Ether/IPv4/UDP|TCP (pkt_ctx_set_fastpath)")
     ap.add_argument("--staging", type=int, default=int(os.environ.get("PKTGPU_STAGING", "0")),
@@ -65,50 +62,8 @@ def parse_args():
                     help="pkt_ctx_set_window bytes (0 = auto)")
     ap.add_argument("--streams", type=int, default=2,
                     help="consecutive steps are issued round-robin on this many HIP streams per device")
-    ap.add_argument("--per-rank", action="store_true",
-                    help="one process per GPU with torch.distributed (the round-2 form) instead of pkt_mgpu")
     ap.add_argument("--no-extra", action="store_true", help="skip the host and pcap records (N = 1)")
     return ap.parse_args()
-
-
-# ------------------------------------------------------------------------------ rank launcher
-def free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
-
-
-def launch_ranks(args):
-    """`bench.py --gpus N` outside torch.distributed.run: start N rank processes, one per device.
-    Nothing here touches the GPU (torch.cuda.device_count() does not initialise it), so the
-    children start from a clean process."""
-    import torch
-    ndev = torch.cuda.device_count()
-    if ndev == 0 or (args.backend == "nccl" and ndev < args.gpus):
-        print(f"bench.py: --gpus {args.gpus} but only {ndev} device(s) visible", file=sys.stderr)
-        return 2
-    port = free_port()
-    procs = []
-    for r in range(args.gpus):
-        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
-                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rc = 0
-    live = list(procs)
-    while live:
-        for p in list(live):
-            code = p.poll()
-            if code is None:
-                continue
-            live.remove(p)
-            if code != 0 and rc == 0:
-                rc = code if code > 0 else 1
-                for q in live:  # one rank failed: the others would wait forever in a collective
-                    q.kill()
-        time.sleep(0.05)
-    return rc
 
 
 # ------------------------------------------------------------------------------ inputs
@@ -249,92 +204,6 @@ def event_avg_ms(torch, stream, launch, reps):
     b.record(stream)
     torch.cuda.synchronize()
     return a.elapsed_time(b) / reps
-
-
-def max_over_ranks(torch, dist, world, x, dev, backend):
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device=dev if backend == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
-
-
-def sync_barrier(torch, dist, world):
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-
-
-def run_c5(args, torch, dist, P, world, rank, dev, cols, d_first, entry):
-    """C5: args.total_packets 64-B packets split in contiguous shards over the ranks (strong
-    scaling), timed like the main loop; then the RCCL gather of one step's packed shard tuples to
-    rank 0 (dist.gather of each rank's single packed buffer), timed separately."""
-    from pktgpu import dist as pdist
-    lo, hi = pdist.shard_range(args.total_packets, world, rank)
-    n5 = hi - lo
-    # the shard: the rank's seeded C2 slab repeated (the parse cost depends only on the layout)
-    reps = -(-n5 // (d_first.numel() // 64))
-    base = d_first.repeat(reps)[:n5 * 64].contiguous()
-    ring = max(2, int(np.ceil((1 << 30) / max(1, base.numel()))))
-    slabs = [base] + [base.clone() for _ in range(ring - 1)]
-    outs = packed_outputs(torch, dev, cols, n5, ring)
-    batches = [P._batch(s, n5, 64, None, None) for s in slabs]
-    ostr = [P.out_struct(o[1]) for o in outs]
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
-    K = max(4, min(args.steps, 40))
-
-    def step(k):
-        P.launch(batches[k % ring], entry, ostr[k % ring], streams[k % len(streams)])
-
-    for k in range(2 * ring):
-        step(k)
-    sync_barrier(torch, dist, world)
-    t0 = time.perf_counter()
-    for k in range(K):
-        step(k)
-    sync_barrier(torch, dist, world)
-    el = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev, args.backend)
-    rec = {"workload": f"C5: {args.total_packets} x 64 B Ether/IPv4/UDP, contiguous shards over {world} GPU(s)",
-           "scaling": "strong", "packets_per_gpu": n5, "steps": K,
-           "ms_per_step": round(el / K * 1e3, 5), "Gpkt/s": round(args.total_packets * K / el / 1e9, 4)}
-    if world > 1:
-        # the used tuple bytes only: the packed buffer's pieces with the batch's used slot rows
-        # (pkt_out_packed_pieces), each padded to the largest shard's for dist.gather
-        from pktgpu import mgpu
-        rows = int(outs[0][1]["n_hdrs"].max().item()) if "n_hdrs" in outs[0][1] else 16
-        rows = int(max_over_ranks(torch, dist, world, rows, dev, args.backend))
-        nmax = pdist.shard_range(args.total_packets, world, 0)[1]  # shard 0 is the largest
-        po, pl = mgpu.packed_pieces(cols, n5, rows)
-        _, plmax = mgpu.packed_pieces(cols, nmax, rows)
-        src = outs[0][0] if args.backend == "nccl" else outs[0][0].cpu()
-        bufs = []
-        for k in range(len(po)):
-            b = torch.zeros(plmax[k], dtype=torch.uint8, device=src.device)
-            b[:pl[k]] = src[po[k]:po[k] + pl[k]]
-            bufs.append(b)
-        glists = [[torch.empty_like(b) for _ in range(world)] if rank == 0 else None for b in bufs]
-
-        def gather():
-            for b, gl in zip(bufs, glists):
-                dist.gather(b, gl, dst=0)
-
-        gather()  # warm (communicator + channels)
-        sync_barrier(torch, dist, world)
-        G = 5
-        tg = time.perf_counter()
-        for _ in range(G):
-            gather()
-        sync_barrier(torch, dist, world)
-        gs = max_over_ranks(torch, dist, world, (time.perf_counter() - tg) / G, dev, args.backend)
-        into_root = sum(b.numel() for b in bufs) * (world - 1)
-        rec["gather"] = {"ms": round(gs * 1e3, 4), "bytes_into_root": into_root,
-                         "GB/s_into_root": round(into_root / gs / 1e9, 2),
-                         "message": f"the packed tuple buffer's {len(bufs)} used piece(s) per rank "
-                                    f"({rows} slot rows, pkt_out_packed_pieces)",
-                         "backend": "nccl (RCCL over xGMI)" if args.backend == "nccl" else args.backend,
-                         "parse_plus_gather_ms": round(el / K * 1e3 + gs * 1e3, 4)}
-    return rec
 
 
 # ------------------------------------------------------------------------------ shared pieces
@@ -670,53 +539,64 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
     rec = {"workload": f"C5: {args.total_packets} x 64 B Ether/IPv4/UDP, contiguous shards over {nd} GPU(s)",
            "scaling": "strong", "packets_per_gpu": [s[0][1] for s in shards], "steps": K,
            "ms_per_step": round(el / K * 1e3, 5), "Gpkt/s": round(args.total_packets * K / el / 1e9, 4)}
-    # parse + gather (one step, blocking), and the parse alone the same way
+    # parse + gather (one step, blocking), and the parse alone the same way; the gather twice: every
+    # piece through RCCL (pkt_mgpu_set_root_copy(0): the root's own shard by ncclSend/ncclRecv to
+    # itself, so RCCL moves bytes at N = 1 too), and the root's own pieces by device copy (default)
     one = [shards[i][0] for i in range(nd)]
     recv = torch.empty(MP.recv_bytes(one, cols, False), dtype=torch.uint8, device=MP.torch_devices[0])
     sh_out = [outs[i][0] for i in range(nd)]
-    MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)  # warm (RCCL channels)
-    MP.synchronize()
-    tp, tg = [], []
-    for _ in range(9):
-        t0 = time.perf_counter()
-        MP.parse(one, columns=cols, shard_out=sh_out)
+
+    def timed_gather(root_copy):
+        MP.set_root_copy(root_copy)
+        MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)  # warm (RCCL channels)
         MP.synchronize()
-        tp.append(time.perf_counter() - t0)
-        t0 = time.perf_counter()
-        MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)
-        MP.synchronize()
-        tg.append(time.perf_counter() - t0)
-    parse_s, pg_s = float(np.median(tp)), float(np.median(tg))
+        tp, tg = [], []
+        for _ in range(9):
+            t0 = time.perf_counter()
+            MP.parse(one, columns=cols, shard_out=sh_out)
+            MP.synchronize()
+            tp.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)
+            MP.synchronize()
+            tg.append(time.perf_counter() - t0)
+        MP.set_root_copy(True)
+        return float(np.median(tp)), float(np.median(tg)), max(min(tg) - min(tp), 1e-9)
+
+    parse_s, pg_s, gmin_s = timed_gather(False)
+    parse_c, pg_c, _ = timed_gather(True)
     rows = int(max(int(o["n_hdrs"].max().item()) for o in
                    [mgpu.packed_views(sh_out[i], cols, one[i][1]) for i in range(nd)]))
-    moved = []
-    for i in range(nd):
-        po, pl = mgpu.packed_pieces(cols, one[i][1], rows)
-        moved.append(sum(pl))
-    into_root = sum(moved[1:])
+    plan, _ = mgpu.gather_plan(cols, [sh[1] for sh in one], [rows] * nd, False)
+    moved = [sum(p[3] for p in plan if p[0] == i) for i in range(nd)]
     gather_s = max(pg_s - parse_s, 1e-9)
-    rec["gather"] = {"entry": "pkt_mgpu_parse_gather (merge = 0, root = device 0)",
+    gather_c = max(pg_c - parse_c, 1e-9)
+    rec["gather"] = {"entry": "pkt_mgpu_parse_gather (merge = 0, root = device 0, pkt_mgpu_set_root_copy(0): "
+                              "every shard's pieces, the root's own included, by grouped ncclSend/ncclRecv)",
                      "parse_ms": round(parse_s * 1e3, 4), "parse_plus_gather_ms": round(pg_s * 1e3, 4),
                      "gather_ms": round(gather_s * 1e3, 4),
-                     "gather_min_ms": round(max(min(tg) - min(tp), 1e-9) * 1e3, 4),
+                     "gather_min_ms": round(gmin_s * 1e3, 4),
                      "bytes_per_pkt_moved": round(sum(moved) / args.total_packets, 2),
                      "slot_rows_moved": rows,
-                     "bytes_into_root": into_root,
-                     "GB/s_into_root": round(into_root / gather_s / 1e9, 2) if into_root else None,
-                     "bytes_root_local": moved[0],
-                     "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI); the root's own shard "
-                                "by hipMemcpyAsync on the root stream",
+                     "bytes_into_root": sum(moved),
+                     "bytes_from_other_devices": sum(moved) - moved[0],
+                     "GB/s_into_root": round(sum(moved) / gather_s / 1e9, 2),
+                     "rccl_messages": len(plan),
+                     "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI; at N = 1 the root's "
+                                "send to itself)",
+                     "root_copy": {"gather_ms": round(gather_c * 1e3, 4),
+                                   "parse_plus_gather_ms": round(pg_c * 1e3, 4),
+                                   "what": "pkt_mgpu_set_root_copy(1), the default: the root's own pieces by "
+                                           "hipMemcpyAsync on the root stream, the others by RCCL"},
                      "timing": "wall clock around each blocking call (+ synchronize), median of 9 "
-                               "(min: gather_min_ms); gather = (parse + gather) - parse, which includes "
-                               "the call's blocking pkt_chain_max_hdrs (used slot rows) before the copies"}
+                               "(min: gather_min_ms); gather = (parse + gather) - parse; the call's slot-row count "
+                               "is reduced inside the parse kernel and read back once per device"}
     return rec
 
 
 # ------------------------------------------------------------------------------ entry
 def main():
     args = parse_args()
-    if args.per_rank:
-        return main_per_rank(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     ndev = world if world > 1 else args.gpus
@@ -740,236 +620,6 @@ def main():
             dist.barrier()
             dist.destroy_process_group()
     print(json.dumps(res), flush=True)
-
-
-# ------------------------------------------------------------------------------ one process per GPU (--per-rank)
-def main_per_rank(args):
-    """The round-2 form: one process per GPU (bench.py spawns them, or torch.distributed.run), every
-    rank parses its own batch per step through the single-device entry, max over ranks."""
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
-    import torch
-    import torch.distributed as dist
-    ndev = torch.cuda.device_count()
-    if ndev == 0:
-        print("bench.py: no GPU visible", file=sys.stderr)
-        sys.exit(2)
-    if args.backend == "nccl" and ndev < world:
-        print(f"bench.py: {world} ranks but only {ndev} device(s) visible", file=sys.stderr)
-        sys.exit(2)
-    gpu = local % ndev  # gloo rehearsal only: several ranks may share one device
-    torch.cuda.set_device(gpu)
-    if world > 1:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
-        else:
-            dist.init_process_group(args.backend)
-    dev = torch.device("cuda", gpu)
-
-    import pktgpu
-    from pktgpu import schema
-    P = pktgpu.Parser(gpu)
-    P.set_fastpath(args.fastpath)
-    P.set_staging(args.staging)
-    P.set_window(args.window)
-    default_cols = {"c2": "chain,ether,ipv4,udp", "c3": "chain,ether,vlan,ipv4,tcp,udp",
-                    "c4": "all", "c5": "chain,ether,ipv4,udp"}[args.config]
-    if args.columns is None:
-        args.columns = default_cols
-    cols = pktgpu.resolve_columns("all" if args.columns == "all" else args.columns.split(","))
-    n = args.packets
-    if args.config == "c5":  # strong scaling: this rank's contiguous block of the global batch
-        from pktgpu import dist as pdist
-        lo, hi = pdist.shard_range(args.total_packets, world, rank)
-        n = hi - lo
-
-    # ---------------- input: one seeded batch per rank, replicated over a >= ring_gib ring
-    slab_np, stride, offs_np, lens_np = make_input(args.config, n, seed=0x5EED0000 + 2 + rank)
-    slab_bytes = slab_np.size
-    ring = max(2, int(np.ceil(args.ring_gib * (1 << 30) / slab_bytes)))
-    d_first = torch.from_numpy(slab_np).to(dev)
-    slabs = [d_first] + [d_first.clone() for _ in range(ring - 1)]
-    d_offs = torch.from_numpy(offs_np).to(dev) if offs_np is not None else None
-    d_lens = torch.from_numpy(lens_np).to(dev) if lens_np is not None else None
-    outs = packed_outputs(torch, dev, cols, n, ring)
-    entry = schema.ENTRY_ID["parse"]
-    batches = [P._batch(slabs[r], n, stride, d_offs, d_lens) for r in range(ring)]
-    ostructs = [P.out_struct(outs[r][1]) for r in range(ring)]
-    streams = [torch.cuda.Stream(dev) for _ in range(max(1, args.streams))]
-
-    def step(k):
-        P.launch(batches[k % ring], entry, ostructs[k % ring], streams[k % len(streams)])
-
-    for k in range(args.warmup):
-        step(k)
-    sync_barrier(torch, dist, world)
-
-    # ---------------- timed region: K steps round-robin over the streams (step k+1 may start
-    # while step k drains).  One event pair brackets the region on stream 0, which joins the others.
-    s0 = streams[0]
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    t0 = time.perf_counter()
-    e0.record(s0)
-    for s_ in streams[1:]:
-        s_.wait_stream(s0)
-    for k in range(args.steps):
-        step(args.warmup + k)
-    for s_ in streams[1:]:
-        s0.wait_stream(s_)
-    e1.record(s0)
-    sync_barrier(torch, dist, world)
-    elapsed = max_over_ranks(torch, dist, world, time.perf_counter() - t0, dev, args.backend)
-    region_ms = e0.elapsed_time(e1)
-
-    # ---------------- roofline sub-phase: the parse kernel in isolation — R back-to-back launches
-    # on ONE stream between one event pair on that stream — alternated with the ceiling probe
-    # (same launch shape, same bytes, no parsing; C2-shaped configs only).  Median of 5 rounds.
-    R = min(args.steps, 50)
-    rs = streams[0]
-    probe = load_probe() if (args.config in ("c2", "c5") and args.columns == default_cols) else None
-
-    def parse_launch(k, s):
-        P.launch(batches[k % ring], entry, ostructs[k % ring], s)
-
-    def probe_launch(k, s):
-        import ctypes
-        rc = probe.pkt_probe_ceiling(ctypes.c_void_p(slabs[k % ring].data_ptr()), n, stride,
-                                     ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
-        if rc != 0:
-            raise RuntimeError(f"pkt_probe_ceiling failed ({rc})")
-
-    # the practical HBM rate of this box: a device copy of the slab (read + write), same ring
-    copy_dst = torch.empty_like(d_first)
-
-    def copy_launch(k, s):
-        with torch.cuda.stream(s):
-            copy_dst.copy_(slabs[k % ring])
-
-    kern, ceil_, copy_ = [], [], []
-    for _ in range(5):
-        kern.append(event_avg_ms(torch, rs, parse_launch, R))
-        if probe is not None:
-            ceil_.append(event_avg_ms(torch, rs, probe_launch, R))
-        copy_.append(event_avg_ms(torch, rs, copy_launch, R))
-    del copy_dst
-    # the probe overwrote output sets: re-parse them so the last step's columns are real
-    for r in range(ring):
-        parse_launch(r, rs)
-    torch.cuda.synchronize()
-
-    c5 = None
-    if args.config == "c2" and not args.no_c5:
-        c5 = run_c5(args, torch, dist, P, world, rank, dev, cols, d_first, entry)
-
-    if rank != 0:
-        if world > 1:
-            dist.destroy_process_group()
-        return
-
-    o0 = outs[0][1]
-    used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
-    span = o0["payload_off"].cpu().numpy() if "payload_off" in o0 else np.full(n, 64, np.int64)
-    read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
-    algo = read_b + write_b
-    avg_kern_s = float(np.median(kern)) * 1e-3
-    achieved = algo / avg_kern_s / 1e9
-    pkts_total = n * world * args.steps  # c5: = total_packets * steps (even shards)
-    value = pkts_total / elapsed / 1e9
-    pipe_s = region_ms * 1e-3 / args.steps
-    agg_gbs = algo * world * args.steps / elapsed / 1e9
-    res = {
-        "metric": METRIC,
-        "value": round(value, 4),
-        "unit": "Gpkt/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": round(elapsed / args.steps * 1e3, 5),
-        "higher_is_better": True,
-        "scaling": "strong" if args.config == "c5" else "weak",
-        "vs_baseline": None,
-        "dtype": "u8",
-        "data": "synthetic (seeded generator, pktgpu/gen.py)",
-        "config": {
-            "workload": {"c2": "C2: 2^20 x 64 B Ether/IPv4/UDP fixed-stride slab per GPU",
-                         "c5": f"C5: {args.total_packets} x 64 B Ether/IPv4/UDP sharded over {world} GPU(s)",
-                         "c3": "C3: 2^20 x 128 B Ether/{0-2}xVlan/IPv4/TCP|UDP per GPU",
-                         "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}[args.config],
-            "packets_per_gpu": n, "entry": "fast::parse", "columns": args.columns,
-            "ring_slabs": ring, "ring_bytes": ring * slab_bytes, "parallelism": f"dp{world}",
-            "staging": args.staging, "window": args.window,
-        },
-        "GB/s": {"algorithmic": round(agg_gbs, 2),
-                 "slab": round(slab_bytes * world * args.steps / elapsed / 1e9, 2),
-                 "algorithmic_bytes_per_pkt": {"read": read_b / n, "written": write_b / n},
-                 "aggregate_frac_of_n_x_peak": round(agg_gbs / (world * HBM_PEAK_GBS), 4)},
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                     "frac_kind": "kernel: algorithmic bytes / isolated launch duration (HIP events, "
-                                  "one stream) / 8 TB/s spec",
-                     "kernel": "parse_kernel", "avg_kernel_us": round(avg_kern_s * 1e6, 3),
-                     "read_only_frac": round(read_b / avg_kern_s / 1e9 / HBM_PEAK_GBS, 4),
-                     "measured": f"median of 5 rounds of {R} back-to-back launches on one stream, one "
-                                 f"HIP event pair per round",
-                     "algorithmic_bytes_per_launch": algo,
-                     # the timed region: K launches pipelined over `streams` streams
-                     "pipelined": {"streams": len(streams),
-                                   "device_ms_per_step": round(pipe_s * 1e3, 5),
-                                   "achieved": round(algo / pipe_s / 1e9, 2),
-                                   "frac": round(algo / pipe_s / 1e9 / HBM_PEAK_GBS, 4),
-                                   "frac_kind": "throughput: algorithmic bytes per step / device time "
-                                                "per step of the pipelined timed region / 8 TB/s"}},
-    }
-    if ceil_:
-        cs = float(np.median(ceil_)) * 1e-3
-        res["roofline"]["ceiling"] = {
-            "kernel": "pkt_probe_ceiling (libpktprobe.so): same launch shape and bytes, no parsing",
-            "avg_kernel_us": round(cs * 1e6, 3), "achieved": round(algo / cs / 1e9, 2),
-            "frac_of_peak": round(algo / cs / 1e9 / HBM_PEAK_GBS, 4),
-            "parse_frac_of_ceiling": round(cs / avg_kern_s, 4)}
-    # the line-granular floor: distinct 128-B lines holding header bytes + the batch index read
-    # + the columns written, priced at this box's measured copy rate (DESIGN.md §5)
-    idx_b = 12 * n if offs_np is not None else 0
-    floor_b = line_bytes(n, stride, offs_np, span) + idx_b + write_b
-    copy_gbs = 2 * slab_bytes / (float(np.median(copy_)) * 1e-3) / 1e9
-    floor_s = floor_b / (copy_gbs * 1e9)
-    res["roofline"]["line_floor"] = {
-        "bytes_per_launch": floor_b, "read_lines": floor_b - idx_b - write_b, "index_read": idx_b,
-        "written": write_b, "copy_rate_GBps": round(copy_gbs, 2),
-        "copy": "torch copy_ of the slab over the same ring (read + write), HIP events, one stream",
-        "floor_us_at_copy_rate": round(floor_s * 1e6, 3),
-        "kernel_frac_of_floor": round(floor_s / avg_kern_s, 4),
-        "pipelined_frac_of_floor": round(floor_s / pipe_s, 4)}
-    # HBM traffic per launch from the committed rocprofv3 PMC passes of this config, if any
-    tpath = os.path.join(REPO, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath) and args.columns == default_cols and n == 1 << 20:
-        t = json.load(open(tpath))
-        res["roofline"]["traffic"] = t["traffic_bytes_per_launch"]
-        res["roofline"]["traffic_source"] = {
-            "measured_in_this_run": False,
-            "file": f"profiles/traffic_{args.config}.json",
-            "how": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes of "
-                   "this bench command (scripts/gpu_round.sh)",
-            "x2_check": "every memory-side read request of these launches is a 128-B line "
-                        "(TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; FETCH_SIZE counts 64 B per request): "
-                        "profiles/ab/r02calib_fetch_requests.txt",
-            "run": t.get("label", "")}
-    if c5 is not None:
-        res["c5"] = c5
-    if world == 1 and not args.no_cpu_baseline:
-        cores, aff, quota = host_cores()
-        threads = args.cpu_threads or cores
-        res["cpu_baseline"] = cpu_baseline(slab_np, stride, offs_np, lens_np, n, cols, threads)
-        res["cpu_baseline"]["host"] = {"affinity_cpus": aff, "cgroup_cpu_quota": quota,
-                                       "os_cpu_count": os.cpu_count()}
-    print(json.dumps(res), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
 
 
 if __name__ == "__main__":

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define PKTGPU_ABI_VERSION 4
+#define PKTGPU_ABI_VERSION 5
 
 /* Maximum number of headers recorded per packet.  The reference recursion is unbounded
  * (fast.rs:53 VLAN stacks, :69 MPLS stacks, :89/:92/:104/:107 IP-in-IP, :168/:186/:219
@@ -259,9 +259,8 @@ int         pkt_ctx_set_fastpath(pkt_ctx_t *ctx, int enable);
 /* Tuning knob: how packet bytes reach LDS.  0 = automatic (currently 1), 1 = per-lane windows of
  * pkt_ctx_set_window bytes (deeper headers read through L2), 2 = wave spans: each wave of 64
  * packets copies the contiguous byte range its packets occupy (up to 16 KiB; else per-lane
- * windows) into LDS by LDS-DMA and walks every header from there, 3 = pipelined windows (windows
- * of >= 64 bytes): persistent waves, each loading its next tile's windows while it walks the
- * current one.  Results are identical in every mode. */
+ * windows) into LDS by LDS-DMA and walks every header from there.  Results are identical in every
+ * mode.  Any other value is PKT_ERR_INVALID_ARG. */
 int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 
 /* Tuning knob: walk schedule.  0 = automatic (lockstep for indexed batches, waterfall for fixed
@@ -428,6 +427,17 @@ uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
  * `stream`).  One such call at a time per ctx. */
 int pkt_chain_max_hdrs(pkt_ctx_t *ctx, const uint8_t *n_hdrs, uint64_t n, uint32_t *max_out, void *stream);
 
+/* PacketSlice of packet i of a parsed batch whose chain columns are in HOST memory (pkt_parse_host's
+ * output, or device columns copied back): for k < *n_hdrs, types[k] / offs[k] = the k-th header of
+ * the PacketSlice's list (its type id and its byte offset in the packet: the Slice the reference's
+ * `insert` put at position k, lib.rs:136-140, packet.rs:724-726), and the payload is packet bytes
+ * [*payload_off, *payload_off + *payload_len) (`set_payload`, packet.rs:728-731).  `out` must hold
+ * status, n_hdrs, hdr_type, hdr_off, payload_off and payload_len (slot columns strided by n).  Returns
+ * the packet's pkt_status_t (>= 0; on a status other than PKT_OK the reference panicked, there is no
+ * PacketSlice, and *n_hdrs = *payload_off = *payload_len = 0), or PKT_ERR_INVALID_ARG.  Host only. */
+int pkt_view(const pkt_out_t *out, uint64_t n, uint64_t i, uint8_t types[PKT_MAX_HDRS],
+             uint16_t offs[PKT_MAX_HDRS], uint32_t *n_hdrs, uint16_t *payload_off, uint16_t *payload_len);
+
 /* ---- packed output buffers (host only, no device needed) ----
  * A column mask selects pkt_out_t members: bit k = the k-th pointer of pkt_out_t (0 = status,
  * ..., 48 = udp_checksum).  The packed layout puts every selected column of an n-packet output in
@@ -459,6 +469,24 @@ uint64_t pkt_out_mask(const pkt_out_t *out);
  * at most one (the lower shards take the remainder). */
 int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t *lo, uint64_t *hi);
 
+/* The gather plan of pkt_mgpu_parse_gather (host only): one piece per message — `bytes` bytes from
+ * offset `src` of shard `shard`'s packed buffer to offset `dst` of the root's receive buffer — for
+ * `nshards` shards of n[i] packets whose batches use rows[i] (<= PKT_MAX_HDRS; rows NULL = all 16)
+ * slot rows.  merge = 0: shard i's packed buffer (its used slot rows only, pkt_out_packed_pieces) at
+ * the next 256-byte boundary of recv; merge = 1: recv is ONE packed output of sum(n) packets (each
+ * column of shard i at packets [lo_i, lo_i + n_i), one piece per column and per used slot row).
+ * Writes min(cap, count) pieces, *npieces = count, *recv_bytes = the receive buffer size. */
+typedef struct pkt_gather_piece {
+    uint64_t src;
+    uint64_t dst;
+    uint64_t bytes;
+    int32_t  shard;
+    uint32_t reserved;
+} pkt_gather_piece_t;
+size_t pkt_sizeof_gather_piece(void);
+int pkt_gather_plan(uint64_t col_mask, int nshards, const uint64_t *n, const uint32_t *rows, int merge,
+                    pkt_gather_piece_t *pieces, uint64_t cap, uint64_t *npieces, uint64_t *recv_bytes);
+
 /* ---- multi-GPU: one process drives several devices ----
  * Every fast::parse_* is a pure function of one packet (fast.rs:5-227), so a batch splits into
  * contiguous shards, one per device, with no exchange inside the parse.  The only collective is
@@ -488,21 +516,21 @@ int pkt_mgpu_parse(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64
  * rate scales with the device count.  Asynchronous: returns after the launches. */
 int pkt_mgpu_parse_steps(pkt_mgpu_t *mg, const pkt_batch_t *batches, int steps, int entry, uint64_t col_mask,
                          void *const *shard_out, int streams);
+/* How the root's own pieces move in pkt_mgpu_gather / pkt_mgpu_parse_gather: 1 (default) = device
+ * copies on the root's stream (an RCCL send to itself moved ~1 TB/s, the copy ~2 TB/s), 0 = RCCL
+ * ncclSend / ncclRecv to itself inside the group like every other shard. */
+int pkt_mgpu_set_root_copy(pkt_mgpu_t *mg, int enable);
 /* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
  * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.
- * Grouped ncclSend/ncclRecv from the other devices; the root's own block is a device copy on the
- * root's stream (an RCCL send to itself moved ~1 TB/s, the copy ~2 TB/s). */
+ * Grouped ncclSend/ncclRecv from the other devices; the root's own block per pkt_mgpu_set_root_copy. */
 int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uint64_t *bytes,
                     void *recv, uint64_t recv_len, const uint64_t *recv_off);
-/* pkt_mgpu_parse, then the gather of every shard's packed tuple buffer into `recv` on the root
- * (consecutive 256-B aligned blocks, each laid out as that shard's packed buffer).  Only the used
- * slot rows move (pkt_chain_max_hdrs of each shard when n_hdrs is among the columns, so the call
- * waits for the parses before it queues the gather; all 16 rows otherwise).  root_views (host array of ndev pkt_out_t, may be NULL)
- * receives the column pointers of each shard's tuples inside `recv`.  With `merge` = 1 the
- * tuples land as ONE packed output of sum(n) packets instead (recv = pkt_out_packed(col_mask,
- * sum n) bytes, shards in order: what pkt_parse_batch over the whole batch would write); the
- * gather then sends each column (each slot row) of a shard as its own message, and root_views[0]
- * receives that single view.  The root's own pieces are device copies, as in pkt_mgpu_gather. */
+/* pkt_mgpu_parse, then the gather of pkt_gather_plan(col_mask, ndev, n, rows, merge) into `recv` on
+ * the root (recv_len >= its recv_bytes), where rows[i] = shard i's largest n_hdrs when n_hdrs is among
+ * the columns (reduced inside each shard's parse kernel; the host waits once per device, after every
+ * parse is queued), else all 16.  root_views (host array of ndev pkt_out_t, may be NULL) receives the
+ * column pointers of each shard's tuples inside `recv` (merge = 0), or root_views[0] the single view
+ * of the whole batch (merge = 1: what pkt_parse_batch over the whole batch would write). */
 int pkt_mgpu_parse_gather(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
                           void *const *shard_out, int root, void *recv, uint64_t recv_len,
                           int merge, pkt_out_t *root_views);

@@ -441,6 +441,10 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         if (fast) fast_result(r, fv);
     }
     PKT_STAMP(2);
+    if (p.nh_max) {  // wave-uniform: the used slot rows of the batch, for a gather of its chain
+        const uint32_t m = wave_max_u32((active_own && r.status == PKT_OK) ? r.n : 0u);
+        if ((t & 63u) == 0 && m) atomicMax(p.nh_max, m);
+    }
     if (active_own) {
         // (the column bases stay in SGPRs from the kernel start: C4 all columns keeps 106 SGPRs and
         // spills 48 to VGPR lanes, ~96 lane instructions per wave; loading them after the walk
@@ -547,127 +551,25 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     auto push = [&](uint32_t slot, uint32_t ty, uint32_t o) { push_slot<GM>(out, ns, slot, i, ty, o); };
     WalkResult r;
     walk<WK>(pv, entry_state(p.entry), active, push, r, T);
+    if (p.nh_max) {
+        const uint32_t m = wave_max_u32((active && r.status == PKT_OK) ? r.n : 0u);
+        if (lane == 0 && m) atomicMax(p.nh_max, m);
+    }
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
     emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
 }
 
 
-// ---- pipelined windows (pkt_ctx_set_staging 3): persistent waves, the next tile's windows in
-// flight while the current tile is walked ----
-// A wave walks tile t out of LDS while the cooperative loads of its next tile t + W (W = waves in
-// the grid) land in registers, and the packet ranges of tile t + 2W are loaded one iteration ahead
-// of those, so every wave always has memory in flight: the wide windows (all headers of the
-// templates in LDS, no dependent global read in the walk or the emit) cost LDS per wave, and the
-// waves the LDS allows must not sit idle during their loads.
-template <int NCH>
-__device__ __forceinline__ void tile_range(const KParams& p, uint32_t tile, uint32_t wl, uint64_t& off, uint32_t& len) {
-    off = 0;
-    len = 0;
-    const uint32_t i = tile * 64u + wl;
-    if (i < p.n) packet_range(p, i, off, len);
-}
-
-template <int NCH>
-__device__ __forceinline__ void tile_chunks(const KParams& p, uint32_t wl, uint64_t off, uint32_t len,
-                                            u32x4 (&ch)[NCH]) {
-    const uint64_t last16 = ((p.slab_len + 15) & ~(uint64_t)15) - 16;
-#pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
-        const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
-        const uint64_t offr = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(off >> 32), (int)r, 64) << 32) |
-                              (uint32_t)__shfl((int)(uint32_t)off, (int)r, 64);
-        const uint32_t lenr = (uint32_t)__shfl((int)len, (int)r, 64);
-        uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
-        a = a > last16 ? last16 : a;
-        ch[k] = u32x4{0, 0, 0, 0};
-        if (16u * c < (uint32_t)(offr & 15) + lenr) ch[k] = *reinterpret_cast<const u32x4*>(p.slab + a);
-    }
-}
-
-template <int NCH>
-__device__ __forceinline__ void tile_stage(uint8_t* lds, uint32_t wl, uint32_t wave0, const u32x4 (&ch)[NCH]) {
-#pragma unroll
-    for (uint32_t k = 0; k < (uint32_t)NCH; k++) {
-        const uint32_t pid = 64u * k + wl, r = pid / (uint32_t)NCH, c = pid % (uint32_t)NCH;
-        uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
-        w[0] = ch[k].x;
-        w[1] = ch[k].y;
-        w[2] = ch[k].z;
-        w[3] = ch[k].w;
-    }
-}
-
-// Resident waves per SIMD the pipelined kernel is compiled for (VGPRs hold the next tile's chunks):
-// the most that compile without VGPR spills.  (A spilling build gave the last, partly active tile
-// of a batch wrong chains on some runs — spill slots written under a partial exec mask and read
-// back by the cross-lane chunk assignment — so every instantiation must stay spill-free:
-// `make asm`, build/resource-usage.txt.)
-__host__ __device__ constexpr int pipe_waves_per_eu(int nch, uint32_t gm) {
-    const bool fields = (gm & ~(uint32_t)(G_CHAIN | G_NT)) != 0;
-    return nch >= 9 ? (fields ? 3 : 4) : nch >= 6 ? 4 : nch >= 5 ? (fields ? 4 : 5) : (fields ? 5 : 6);
-}
-template <int NCH, uint32_t GM, int WK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(pipe_waves_per_eu(NCH, GM))))
-void parse_pipe_kernel(KParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
-    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
-    const uint32_t wl = threadIdx.x & 63u, wave0 = threadIdx.x & ~63u;
-    const uint32_t ntiles = (p.n + 63u) / 64u;
-    const uint32_t W = gridDim.x * (uint32_t)kWavesPerBlock;
-    // wave-uniform (an SGPR: the loop and its branches stay scalar, no exec-mask bookkeeping)
-    uint32_t tile = __builtin_amdgcn_readfirstlane(blockIdx.x * (uint32_t)kWavesPerBlock + (threadIdx.x >> 6));
-    uint64_t off, off1, off2;
-    uint32_t len, len1, len2;
-    u32x4 ch[NCH];
-    tile_range<NCH>(p, tile, wl, off, len);
-    tile_chunks<NCH>(p, wl, off, len, ch);
-    tile_range<NCH>(p, tile + W, wl, off1, len1);
-    const u32x4 none[NCH] = {};
-    (void)none;
-    while (tile < ntiles) {
-        // this tile's chunks into the lanes' windows (the previous tile's walk and emit are done)
-        __builtin_amdgcn_wave_barrier();
-        tile_stage<NCH>(lds, wl, wave0, ch);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // the next tile's loads in flight (chunks of tile + W, ranges of tile + 2W)
-        if (tile + W < ntiles) tile_chunks<NCH>(p, wl, off1, len1, ch);
-        tile_range<NCH>(p, tile + 2 * W, wl, off2, len2);
-        // walk and emit this tile from LDS
-        const uint32_t base = tile * 64u - wave0;  // parse_tile's lane index = base + threadIdx.x
-        parse_tile<NCH, GM, WK, true>(p, lds, base, none, off, len, tile * 64u + wl < p.n, pkt_st, T);
-        off = off1;
-        len = len1;
-        off1 = off2;
-        len1 = len2;
-        tile += W;
-    }
-}
-
-// How a launch stages packet bytes: per-lane windows (one tile per block), wave spans, or
-// pipelined windows (persistent waves).
-enum LaunchMode { M_TILE = 0, M_SPAN = 2, M_PIPE = 3 };
+// How a launch stages packet bytes: per-lane windows (one tile per block) or wave spans.
+// (Round 3's pipelined windows — persistent waves loading the next tile's windows into VGPRs while
+// walking the current one — were slower on every measured batch, C4 96.7 vs 89.9 us isolated,
+// profiles/ab/r03b_c4_staging3_pipelined_windows.txt, and correct only while every instantiation
+// stayed spill-free; removed in round 4.)
+enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
 
 template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
-    if constexpr (NCH == 4 || NCH == 6 || NCH == 9) if (mode == M_PIPE) {
-        // persistent: as many blocks as reside on a CU (its LDS over the block's windows, and the
-        // waves per SIMD the kernel is compiled for), at most one wave per tile
-        int cus = 256, dev = 0;
-        (void)hipGetDevice(&dev);
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const uint32_t per_cu = std::max<uint32_t>(
-            1u, std::min<uint32_t>((uint32_t)((160u * 1024u) / with_tables(window_lds(NCH), WK)),
-                                   (uint32_t)(4 * pipe_waves_per_eu(NCH, GM) / kWavesPerBlock)));
-        const uint32_t tiles = (kp.n + 63u) / 64u;
-        const uint32_t blocks = std::max<uint32_t>(1u, std::min<uint32_t>((uint32_t)cus * per_cu, (tiles + kWavesPerBlock - 1) / kWavesPerBlock));
-        hipLaunchKernelGGL((parse_pipe_kernel<NCH, GM, WK>), dim3(blocks), dim3(kBlock),
-                           with_tables(window_lds(NCH), WK), s, kp);
-        return hipGetLastError();
-    }
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), with_tables(span_region(NCH), WK), s, kp);
@@ -895,7 +797,7 @@ int pkt_ctx_set_fastpath(pkt_ctx_t* ctx, int enable) {
 }
 
 int pkt_ctx_set_staging(pkt_ctx_t* ctx, int mode) {
-    if (!ctx || mode < 0 || mode > 3) return PKT_ERR_INVALID_ARG;
+    if (!ctx || mode < 0 || mode > 2) return PKT_ERR_INVALID_ARG;
     ctx->staging = mode;
     return PKT_SUCCESS;
 }
@@ -907,7 +809,7 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
 }
 
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias, int staging);
+                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max = nullptr);
 
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
@@ -916,9 +818,34 @@ int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_o
     return parse_impl(ctx, b, entry, out, stream, 0, ctx ? ctx->staging : 0);
 }
 
+}  // extern "C"
+
+// (internal, pktgpu_ctx.hpp) pkt_parse_batch whose kernel also reduces the batch's largest n_hdrs
+// (a wave max + one atomicMax per wave, fused into the parse) into a ctx word, copied to the ctx's
+// pinned mirror on `stream`: *rows_host holds it once the stream has passed this call.
+int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
+                            const uint32_t** rows_host) {
+    if (!ctx || !rows_host) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (b && b->n && b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = ensure_max_scratch(ctx);
+    if (e != hipSuccess) return hip_fail(ctx, e, "parse rows scratch");
+    const int w = MaxScratch::kWords - 1;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if ((e = hipMemsetAsync(ctx->mx.dev + w, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
+    const int rc = parse_impl(ctx, b, entry, out, stream, 0, ctx->staging, ctx->mx.dev + w);
+    if (rc != PKT_SUCCESS) return rc;
+    if ((e = hipMemcpyAsync(ctx->mx.host + w, ctx->mx.dev + w, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemcpyAsync (rows)");
+    *rows_host = ctx->mx.host + w;
+    return PKT_SUCCESS;
+}
+
+extern "C" {
+
 // `staging` = the ctx's knob, or the host path's override (wave spans over the link).
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias, int staging) {
+                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -952,7 +879,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // Staging: wave spans when asked; per-lane windows otherwise (auto: spans measured slower on
     // device-resident C3 and C4).
-    const int mode = staging == 2 ? M_SPAN : (staging == 3 ? M_PIPE : M_TILE);
+    const int mode = staging == 2 ? M_SPAN : M_TILE;
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
@@ -971,6 +898,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         kp.n = (uint32_t)cnt;
         kp.entry = entry;
         kp.fast = ctx->fast && (entry == PKT_ENTRY_PARSE || entry == PKT_ENTRY_ETHERNET);
+        kp.nh_max = nh_max;
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         for (int c = 0; c < 49; c++)

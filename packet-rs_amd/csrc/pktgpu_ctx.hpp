@@ -23,8 +23,10 @@ struct HostPipe {
 
 // Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.
 struct PcapScratch {
-    void* buf = nullptr;   // the tile ticket + one published state per 16 KiB tile
+    void* buf = nullptr;   // the ticket, nb_cap scan-block states, then k_cap regions' words
     uint64_t bytes = 0;
+    uint32_t k_cap = 0;    // regions the buffer holds (its layout is fixed by k_cap / nb_cap)
+    uint32_t nb_cap = 0;   // scan-block states the buffer holds
     uint64_t* ctl = nullptr;      // pinned host words the indexer reads back (magic, total, error)
     uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the kernel writes them)
     uint32_t epoch = 0;           // per call: block states of older calls are ignored, not cleared
@@ -74,3 +76,9 @@ inline int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
     if (ctx) ctx->err = std::string(what) + ": " + hipGetErrorString(e);
     return PKT_ERR_HIP;
 }
+
+// pkt_parse_batch that also leaves the batch's largest n_hdrs (its used slot rows, <= PKT_MAX_HDRS
+// for a parsed packet) in pinned host memory: *rows_host is valid once `stream` has passed the call.
+// The reduction is fused into the parse kernel.  Used by the multi-GPU gather (pktgpu_mgpu.cpp).
+int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
+                            const uint32_t** rows_host);

@@ -57,7 +57,15 @@ struct KParams {
     int entry;
     int fast;  // register fast path for Ether/IPv4/UDP|TCP (entries PARSE / ETHERNET)
     pkt_out_t out;
+    uint32_t* nh_max;  // non-NULL: atomicMax of the batch's largest n_hdrs (the used slot rows) here
 };
+
+// The largest value of v over the wave (butterfly; every lane gets it).
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, m, 64));
+    return v;
+}
 
 // EtherType dispatch (types.rs:51-75 as matched in fast.rs:38-45 / 52-59)
 __device__ __forceinline__ uint32_t etype_next(uint32_t et) {

@@ -125,6 +125,29 @@ int pkt_pcap_index(const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t
     return PKT_SUCCESS;
 }
 
+// The PacketSlice of packet i from host chain columns (lib.rs:136-140: hdrs in `insert` order,
+// packet.rs:724-731: insert / set_payload).
+int pkt_view(const pkt_out_t* out, uint64_t n, uint64_t i, uint8_t types[PKT_MAX_HDRS], uint16_t offs[PKT_MAX_HDRS],
+             uint32_t* n_hdrs, uint16_t* payload_off, uint16_t* payload_len) {
+    if (!out || !types || !offs || !n_hdrs || !payload_off || !payload_len || i >= n) return PKT_ERR_INVALID_ARG;
+    if (!out->status || !out->n_hdrs || !out->hdr_type || !out->hdr_off || !out->payload_off || !out->payload_len)
+        return PKT_ERR_INVALID_ARG;
+    *n_hdrs = 0;
+    *payload_off = *payload_len = 0;
+    const int st = out->status[i];
+    if (st != PKT_OK) return st;
+    const uint32_t nh = out->n_hdrs[i];
+    if (nh > PKT_MAX_HDRS) return PKT_ERR_INVALID_ARG;
+    for (uint32_t k = 0; k < nh; k++) {
+        types[k] = out->hdr_type[(uint64_t)k * n + i];
+        offs[k] = out->hdr_off[(uint64_t)k * n + i];
+    }
+    *n_hdrs = nh;
+    *payload_off = out->payload_off[i];
+    *payload_len = out->payload_len[i];
+    return st;
+}
+
 // Packet::ipv4_checksum (src/packet.rs:93-107), Q1 fold included.
 uint16_t pkt_ipv4_checksum_host(const uint8_t* v, size_t len) {
     uint32_t s = 0;

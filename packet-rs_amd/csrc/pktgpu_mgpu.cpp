@@ -28,6 +28,8 @@ struct pkt_mgpu {
     // and one event per stream, created on first use
     std::vector<hipStream_t> xs;  // [ndev][kMaxStreams - 1]
     std::vector<hipEvent_t> xe;   // [ndev][kMaxStreams]
+    bool xinit = false;           // xs / xe all created (set only after every creation succeeded)
+    int root_copy = 1;            // the root's own pieces: 1 = hipMemcpyAsync, 0 = RCCL send/recv to itself
     std::string err;
 };
 
@@ -95,28 +97,54 @@ int packed_pieces(uint64_t mask, uint64_t n, uint32_t rows, uint64_t off[2], uin
     return 1;
 }
 
-// Merged gather plan: (source offset in the shard buffer, destination offset in the root
-// buffer, bytes) of each message — one per column, one per slot row for slot columns.
-struct Piece {
-    uint64_t src, dst, bytes;
-};
-void merged_pieces(uint64_t mask, uint64_t n_i, uint64_t lo, uint64_t n_total, uint32_t rows,
-                   std::vector<Piece>& out) {
-    uint64_t so[kNumCols], dof[kNumCols];
-    packed_layout(mask, n_i, so);
-    packed_layout(mask, n_total, dof);
+// The gather plan (pkt_gather_plan): one piece per message, in issue order.
+//   merge = 0: shard i's packed buffer lands at the next 256-B boundary of recv, its used slot rows
+//              only (packed_pieces: at most two messages per shard);
+//   merge = 1: recv is ONE packed output of sum(n) packets (what pkt_parse_batch over the whole
+//              batch writes): each column of shard i at its rows [lo_i, lo_i + n_i), one message per
+//              column and per used slot row.
+// Returns the receive-buffer size.
+uint64_t gather_plan(uint64_t mask, int nd, const uint64_t* n, const uint32_t* rows, int merge,
+                     std::vector<pkt_gather_piece_t>& out) {
     out.clear();
-    if (n_i == 0) return;
-    for (int c = 0; c < kNumCols; c++) {
-        if (!(mask >> c & 1)) continue;
-        const uint64_t esz = kColSize[c];
-        if (c == kColHdrType || c == kColHdrOff) {
-            for (uint64_t j = 0; j < rows; j++)
-                out.push_back({so[c] + j * n_i * esz, dof[c] + (j * n_total + lo) * esz, n_i * esz});
-        } else {
-            out.push_back({so[c], dof[c] + lo * esz, n_i * esz});
+    uint64_t n_total = 0;
+    for (int i = 0; i < nd; i++) n_total += n[i];
+    if (merge) {
+        uint64_t dof[kNumCols], lo = 0;
+        packed_layout(mask, n_total, dof);
+        for (int i = 0; i < nd; i++) {
+            const uint64_t ni = n[i];
+            const uint32_t r = rows ? rows[i] : PKT_MAX_HDRS;
+            if (ni) {
+                uint64_t so[kNumCols];
+                packed_layout(mask, ni, so);
+                for (int c = 0; c < kNumCols; c++) {
+                    if (!(mask >> c & 1)) continue;
+                    const uint64_t esz = kColSize[c];
+                    if (c == kColHdrType || c == kColHdrOff) {
+                        for (uint64_t j = 0; j < r; j++)
+                            out.push_back({so[c] + j * ni * esz, dof[c] + (j * n_total + lo) * esz, ni * esz, i, 0});
+                    } else {
+                        out.push_back({so[c], dof[c] + lo * esz, ni * esz, i, 0});
+                    }
+                }
+            }
+            lo += ni;
         }
+        return packed_layout(mask, n_total, nullptr);
     }
+    uint64_t o = 0, need = 0;
+    for (int i = 0; i < nd; i++) {
+        o = round_up(need);
+        if (n[i]) {
+            uint64_t po[2], pl[2];
+            const int np = packed_pieces(mask, n[i], rows ? rows[i] : PKT_MAX_HDRS, po, pl);
+            for (int k = 0; k < np; k++)
+                if (pl[k]) out.push_back({po[k], o + po[k], pl[k], i, 0});
+        }
+        need = o + packed_layout(mask, n[i], nullptr);
+    }
+    return need;
 }
 
 }  // namespace
@@ -260,17 +288,36 @@ int pkt_mgpu_parse_steps(pkt_mgpu_t* mg, const pkt_batch_t* batches, int steps, 
     const int nd = mg->ndev, S = streams;
     for (int k = 0; k < steps * nd; k++)
         if (batches[k].n && !shard_out[k]) return mfail(mg, PKT_ERR_INVALID_ARG, "null shard output");
-    if (mg->xs.empty()) {  // extra streams and the join events, once
+    if (!mg->xinit) {  // extra streams and the join events, once (all or nothing: retried after a failure)
         mg->xs.assign((size_t)nd * (pkt_mgpu::kMaxStreams - 1), nullptr);
         mg->xe.assign((size_t)nd * pkt_mgpu::kMaxStreams, nullptr);
-        for (int i = 0; i < nd; i++) {
-            hipError_t e = hipSetDevice(mg->dev[i]);
+        hipError_t e = hipSuccess;
+        for (int i = 0; i < nd && e == hipSuccess; i++) {
+            e = hipSetDevice(mg->dev[i]);
             for (int j = 0; j < pkt_mgpu::kMaxStreams - 1 && e == hipSuccess; j++)
                 e = hipStreamCreateWithFlags(&mg->xs[i * (pkt_mgpu::kMaxStreams - 1) + j], hipStreamNonBlocking);
             for (int j = 0; j < pkt_mgpu::kMaxStreams && e == hipSuccess; j++)
                 e = hipEventCreateWithFlags(&mg->xe[i * pkt_mgpu::kMaxStreams + j], hipEventDisableTiming);
-            if (e != hipSuccess) return mhip(mg, e, "pkt_mgpu_parse_steps streams");
         }
+        if (e != hipSuccess) {
+            for (int i = 0; i < nd; i++) {
+                (void)hipSetDevice(mg->dev[i]);
+                for (int j = 0; j < pkt_mgpu::kMaxStreams - 1; j++) {
+                    hipStream_t& x = mg->xs[i * (pkt_mgpu::kMaxStreams - 1) + j];
+                    if (x) (void)hipStreamDestroy(x);
+                    x = nullptr;
+                }
+                for (int j = 0; j < pkt_mgpu::kMaxStreams; j++) {
+                    hipEvent_t& v = mg->xe[i * pkt_mgpu::kMaxStreams + j];
+                    if (v) (void)hipEventDestroy(v);
+                    v = nullptr;
+                }
+            }
+            mg->xs.clear();
+            mg->xe.clear();
+            return mhip(mg, e, "pkt_mgpu_parse_steps streams");
+        }
+        mg->xinit = true;
     }
     // One host thread per device issues that device's launches (one launch per step, round-robin
     // over S streams that first wait for the device's work stream and are joined back into it), so
@@ -318,40 +365,78 @@ int pkt_mgpu_parse_steps(pkt_mgpu_t* mg, const pkt_batch_t* batches, int steps, 
     return PKT_SUCCESS;
 }
 
-int pkt_mgpu_gather(pkt_mgpu_t* mg, int root, const void* const* send, const uint64_t* bytes, void* recv,
-                    uint64_t recv_len, const uint64_t* recv_off) {
-    if (!mg || !send || !bytes) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
-    if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
-    std::vector<uint64_t> off(mg->ndev);
-    uint64_t o = 0;
-    for (int i = 0; i < mg->ndev; i++) {
-        off[i] = recv_off ? recv_off[i] : o;
-        o = round_up(off[i] + bytes[i]);
-        if (bytes[i] && (!send[i] || !recv)) return mfail(mg, PKT_ERR_INVALID_ARG, "null buffer");
-        if (off[i] + bytes[i] > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
-    }
-    // the root's own shard: a device copy on the root stream (an RCCL send to itself moved it at
-    // ~1 TB/s, bench c5 at N = 1)
-    if (bytes[root]) {
+int pkt_gather_plan(uint64_t mask, int nshards, const uint64_t* n, const uint32_t* rows, int merge,
+                    pkt_gather_piece_t* pieces, uint64_t cap, uint64_t* npieces, uint64_t* recv_bytes) {
+    if (mask >> kNumCols || nshards <= 0 || !n || (merge != 0 && merge != 1) || (cap && !pieces))
+        return PKT_ERR_INVALID_ARG;
+    if (rows)
+        for (int i = 0; i < nshards; i++)
+            if (rows[i] > PKT_MAX_HDRS) return PKT_ERR_INVALID_ARG;
+    std::vector<pkt_gather_piece_t> v;
+    const uint64_t rb = gather_plan(mask, nshards, n, rows, merge, v);
+    for (uint64_t k = 0; k < v.size() && k < cap; k++) pieces[k] = v[k];
+    if (npieces) *npieces = v.size();
+    if (recv_bytes) *recv_bytes = rb;
+    return PKT_SUCCESS;
+}
+
+size_t pkt_sizeof_gather_piece(void) { return sizeof(pkt_gather_piece_t); }
+
+int pkt_mgpu_set_root_copy(pkt_mgpu_t* mg, int enable) {
+    if (!mg || enable < 0 || enable > 1) return mfail(mg, PKT_ERR_INVALID_ARG, "bad argument");
+    mg->root_copy = enable;
+    return PKT_SUCCESS;
+}
+
+}  // extern "C"
+
+namespace {
+// Issue a gather plan: each piece from shard p.shard's buffer send[p.shard] + p.src to recv + p.dst
+// on the root.  The root's own pieces are device copies on the root stream (mg->root_copy) or RCCL
+// send/recv to itself; every other piece is a grouped ncclSend (the shard's stream) / ncclRecv (the
+// root's stream).
+int issue_plan(pkt_mgpu* mg, int root, const void* const* send, void* recv, const std::vector<pkt_gather_piece_t>& plan) {
+    if (mg->root_copy) {
         hipError_t e = hipSetDevice(mg->dev[root]);
-        if (e == hipSuccess)
-            e = hipMemcpyAsync(static_cast<uint8_t*>(recv) + off[root], send[root], bytes[root], hipMemcpyDeviceToDevice,
-                               mg->stream[root]);
+        for (const pkt_gather_piece_t& p : plan)
+            if (p.shard == root && e == hipSuccess)
+                e = hipMemcpyAsync(static_cast<uint8_t*>(recv) + p.dst, static_cast<const uint8_t*>(send[root]) + p.src,
+                                   p.bytes, hipMemcpyDeviceToDevice, mg->stream[root]);
         if (e != hipSuccess) return mhip(mg, e, "hipMemcpyAsync (root shard)");
     }
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
-    for (int i = 0; i < mg->ndev && r == ncclSuccess; i++) {
-        if (!bytes[i] || i == root) continue;
-        r = ncclSend(send[i], bytes[i], ncclUint8, root, mg->comm[i], mg->stream[i]);
-        if (r == ncclSuccess)
-            r = ncclRecv(static_cast<uint8_t*>(recv) + off[i], bytes[i], ncclUint8, i, mg->comm[root],
-                         mg->stream[root]);
+    for (const pkt_gather_piece_t& p : plan) {
+        const int i = p.shard;
+        if (i == root && mg->root_copy) continue;
+        r = ncclSend(static_cast<const uint8_t*>(send[i]) + p.src, p.bytes, ncclUint8, root, mg->comm[i], mg->stream[i]);
+        if (r != ncclSuccess) break;
+        r = ncclRecv(static_cast<uint8_t*>(recv) + p.dst, p.bytes, ncclUint8, i, mg->comm[root], mg->stream[root]);
+        if (r != ncclSuccess) break;
     }
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess) return mnccl(mg, r, "ncclSend/ncclRecv");
     if (r2 != ncclSuccess) return mnccl(mg, r2, "ncclGroupEnd");
     return PKT_SUCCESS;
+}
+}  // namespace
+
+extern "C" {
+
+int pkt_mgpu_gather(pkt_mgpu_t* mg, int root, const void* const* send, const uint64_t* bytes, void* recv,
+                    uint64_t recv_len, const uint64_t* recv_off) {
+    if (!mg || !send || !bytes) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
+    if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
+    std::vector<pkt_gather_piece_t> plan;
+    uint64_t o = 0;
+    for (int i = 0; i < mg->ndev; i++) {
+        const uint64_t off = recv_off ? recv_off[i] : o;
+        o = round_up(off + bytes[i]);
+        if (bytes[i] && (!send[i] || !recv)) return mfail(mg, PKT_ERR_INVALID_ARG, "null buffer");
+        if (off + bytes[i] > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
+        if (bytes[i]) plan.push_back({0, off, bytes[i], i, 0});
+    }
+    return issue_plan(mg, root, send, recv, plan);
 }
 
 int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry, uint64_t mask,
@@ -360,75 +445,59 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
     if (!mg || !batches || !shard_out) return mfail(mg, PKT_ERR_INVALID_ARG, "null argument");
     if (root < 0 || root >= mg->ndev) return mfail(mg, PKT_ERR_INVALID_ARG, "bad root");
     if (merge != 0 && merge != 1) return mfail(mg, PKT_ERR_INVALID_ARG, "bad merge flag");
+    if (mask >> kNumCols) return mfail(mg, PKT_ERR_INVALID_ARG, "bad column mask");
     const int nd = mg->ndev;
     // validate the receive buffer before anything is launched or any view is filled in
-    uint64_t n_total = 0, need = 0;
+    std::vector<uint64_t> n(nd);
+    uint64_t n_total = 0;
     for (int i = 0; i < nd; i++) {
-        n_total += batches[i].n;
-        need = round_up(need) + packed_layout(mask, batches[i].n, nullptr);
+        n[i] = batches[i].n;
+        n_total += n[i];
+        if (n[i] && !shard_out[i]) return mfail(mg, PKT_ERR_INVALID_ARG, "null shard output");
     }
-    if (merge) need = packed_layout(mask, n_total, nullptr);
+    std::vector<pkt_gather_piece_t> plan;
+    const uint64_t need = gather_plan(mask, nd, n.data(), nullptr, merge, plan);
     if (n_total && !recv) return mfail(mg, PKT_ERR_INVALID_ARG, "null recv");
     if (need > recv_len) return mfail(mg, PKT_ERR_INVALID_ARG, "recv buffer too small");
-    int rc = pkt_mgpu_parse(mg, batches, entry, mask, shard_out);
-    if (rc != PKT_SUCCESS) return rc;
-    // Slot rows to move per shard: its largest n_hdrs (rows past it hold nothing), found on the
-    // device after the parse (the shards' parses all run while the host waits for the first).
+    // Parse every shard.  Slot rows to move per shard = its largest n_hdrs (rows past it hold
+    // nothing, a PacketSlice holds exactly its headers): reduced inside the parse kernel and copied
+    // to pinned host memory on the shard's stream; the host waits once per device, after every
+    // shard's parse is queued.
+    const bool nh = mask >> 1 & 1;
     std::vector<uint32_t> rows(nd, PKT_MAX_HDRS);
-    if (mask >> 1 & 1) {  // n_hdrs is among the columns
+    std::vector<const uint32_t*> rows_host(nd, nullptr);
+    for (int i = 0; i < nd; i++) {
+        if (!n[i]) continue;
+        pkt_out_t o;
+        pkt_out_packed(mask, n[i], shard_out[i], &o, nullptr);
+        const int rc = nh ? pktgpu_parse_rows_async(mg->ctx[i], &batches[i], entry, &o, mg->stream[i], &rows_host[i])
+                          : pkt_parse_batch(mg->ctx[i], &batches[i], entry, &o, mg->stream[i]);
+        if (rc != PKT_SUCCESS)
+            return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
+    }
+    if (nh) {
         for (int i = 0; i < nd; i++) {
-            if (!batches[i].n) continue;
-            pkt_out_t o;
-            pkt_out_packed(mask, batches[i].n, shard_out[i], &o, nullptr);
-            rc = pkt_chain_max_hdrs(mg->ctx[i], o.n_hdrs, batches[i].n, &rows[i], mg->stream[i]);
-            if (rc != PKT_SUCCESS)
-                return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
+            if (!n[i]) continue;
+            hipError_t e = hipSetDevice(mg->dev[i]);
+            if (e == hipSuccess) e = hipStreamSynchronize(mg->stream[i]);
+            if (e != hipSuccess) return mhip(mg, e, "hipStreamSynchronize (slot rows)");
+            rows[i] = std::min<uint32_t>(*rows_host[i], PKT_MAX_HDRS);
         }
+        gather_plan(mask, nd, n.data(), rows.data(), merge, plan);
     }
-    std::vector<Piece> pieces;
-    uint64_t lo = 0, o = 0;
-    if (merge && root_views) pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
-    ncclResult_t r = ncclGroupStart();
-    if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
-    for (int i = 0; i < nd && r == ncclSuccess; i++) {
+    if (root_views) {
         if (merge) {
-            // each column (each used slot row) of the shard at its place in the whole batch's output
-            merged_pieces(mask, batches[i].n, lo, n_total, rows[i], pieces);
-            lo += batches[i].n;
+            pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
         } else {
-            // the shard's packed buffer at the next 256-B boundary of recv, used slot rows only
-            pieces.clear();
-            if (root_views) pkt_out_packed(mask, batches[i].n, static_cast<uint8_t*>(recv) + o, &root_views[i], nullptr);
-            uint64_t po[2], pl[2];
-            const int np = packed_pieces(mask, batches[i].n, rows[i], po, pl);
-            for (int k = 0; k < np; k++)
-                if (pl[k] && batches[i].n) pieces.push_back({po[k], o + po[k], pl[k]});
-            o = round_up(o + packed_layout(mask, batches[i].n, nullptr));
-        }
-        if (i == root) {  // the root's own pieces: device copies on the root stream (not RCCL)
-            hipError_t e = hipSetDevice(mg->dev[root]);
-            for (const Piece& p : pieces)
-                if (e == hipSuccess)
-                    e = hipMemcpyAsync(static_cast<uint8_t*>(recv) + p.dst, static_cast<const uint8_t*>(shard_out[i]) + p.src,
-                                       p.bytes, hipMemcpyDeviceToDevice, mg->stream[root]);
-            if (e != hipSuccess) {
-                (void)ncclGroupEnd();
-                return mhip(mg, e, "hipMemcpyAsync (root shard)");
+            uint64_t o = 0, end = 0;
+            for (int i = 0; i < nd; i++) {
+                o = round_up(end);
+                pkt_out_packed(mask, n[i], static_cast<uint8_t*>(recv) + o, &root_views[i], nullptr);
+                end = o + packed_layout(mask, n[i], nullptr);
             }
-            continue;
-        }
-        for (const Piece& p : pieces) {
-            r = ncclSend(static_cast<const uint8_t*>(shard_out[i]) + p.src, p.bytes, ncclUint8, root, mg->comm[i],
-                         mg->stream[i]);
-            if (r != ncclSuccess) break;
-            r = ncclRecv(static_cast<uint8_t*>(recv) + p.dst, p.bytes, ncclUint8, i, mg->comm[root], mg->stream[root]);
-            if (r != ncclSuccess) break;
         }
     }
-    const ncclResult_t r2 = ncclGroupEnd();
-    if (r != ncclSuccess) return mnccl(mg, r, "ncclSend/ncclRecv");
-    if (r2 != ncclSuccess) return mnccl(mg, r2, "ncclGroupEnd");
-    return PKT_SUCCESS;
+    return issue_plan(mg, root, shard_out, recv, plan);
 }
 
 int pkt_mgpu_synchronize(pkt_mgpu_t* mg) {

@@ -707,28 +707,34 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
     // Scratch: the ticket, the scan blocks' states, per-region states, prefixes and record lists.
-    const uint64_t need = 64 + (uint64_t)nb * sizeof(BlkDesc) + (uint64_t)K * (8 + 8 + 8 + 4 + 2 * kMaxRec);
+    // The layout is fixed by the ALLOCATED capacity (k_cap regions, nb_cap block states), not by
+    // this call's K: the block-state array must never overlay an earlier call's per-region words
+    // (file positions and prefixes a look-back could take for a state published in this epoch).
     PcapScratch& pc = ctx->pc;
-    if (pc.bytes < need) {
+    if (K > pc.k_cap) {
         if (pc.buf) {
             (void)hipStreamSynchronize(s);
             (void)hipFree(pc.buf);
             pc.buf = nullptr;
             pc.bytes = 0;
+            pc.k_cap = pc.nb_cap = 0;
         }
-        const uint64_t bytes = need + need / 4;
+        const uint32_t kc = K + K / 4 + 64, nbc = (kc + kScanRegions - 1) / kScanRegions;
+        const uint64_t bytes = 64 + (uint64_t)nbc * sizeof(BlkDesc) + (uint64_t)kc * (8 + 8 + 8 + 4 + 2 * kMaxRec);
         e = hipMalloc(&pc.buf, bytes);
         if (e == hipSuccess) e = hipMemsetAsync(pc.buf, 0, bytes, s);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
         pc.bytes = bytes;
+        pc.k_cap = kc;
+        pc.nb_cap = nbc;
     }
     if (!pc.ctl) {
         e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kHostWords, hipHostMallocMapped);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&pc.ctl_dev), pc.ctl, 0);
         if (e != hipSuccess) return hip_fail(ctx, e, "hipHostMalloc (pcap index)");
     }
-    // a new epoch per call (block states of older calls are ignored, not cleared; they may lie
-    // anywhere in the buffer, hence the full reset on wrap)
+    // a new epoch per call (block states of older calls are ignored, not cleared; the block-state
+    // area only ever holds epoch-tagged states, reset in full on wrap)
     if (++pc.epoch >= (1u << 24)) {
         pc.epoch = 1;
         if ((e = hipMemsetAsync(pc.buf, 0, pc.bytes, s)) != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
@@ -737,15 +743,15 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     char* p = static_cast<char*>(pc.buf);
     S.ticket = reinterpret_cast<uint32_t*>(p);
     S.blk = reinterpret_cast<BlkDesc*>(p + 64);
-    p += 64 + (uint64_t)nb * sizeof(BlkDesc);
+    p += 64 + (uint64_t)pc.nb_cap * sizeof(BlkDesc);
     S.rentry = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * K;
+    p += 8ull * pc.k_cap;
     S.rexit = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * K;
+    p += 8ull * pc.k_cap;
     S.rpre = reinterpret_cast<uint64_t*>(p);
-    p += 8ull * K;
+    p += 8ull * pc.k_cap;
     S.rcnt = reinterpret_cast<uint32_t*>(p);
-    p += 4ull * K;
+    p += 4ull * pc.k_cap;
     S.list = reinterpret_cast<uint16_t*>(p);
     S.host = pc.ctl_dev;
     S.epoch = pc.epoch;

@@ -25,7 +25,7 @@ from . import schema
 from .schema import (ABI_VERSION, DEPTH_LIMIT, ENTRIES, ENTRY_ID, GROUPS, HDR_ID, HDR_NAMES,  # noqa: F401
                      HDR_SIZES, MAX_HDRS, OK, STATUS_NAMES, TRUNCATED)
 
-__all__ = ["Parser", "packet_slice", "PacketSlice", "HeaderSlice", "resolve_columns", "schema"]
+__all__ = ["Parser", "packet_slice", "view", "PacketSlice", "HeaderSlice", "resolve_columns", "schema"]
 
 
 def resolve_columns(columns):
@@ -104,7 +104,7 @@ class Parser:
         self._check(self._L.pkt_ctx_set_fastpath(self._ctx, int(bool(enable))), "pkt_ctx_set_fastpath")
 
     def set_staging(self, mode):
-        """0 = auto, 1 = per-lane windows, 2 = wave spans, 3 = pipelined windows (pkt_ctx_set_staging)."""
+        """0 = auto, 1 = per-lane windows, 2 = wave spans (pkt_ctx_set_staging)."""
         self._check(self._L.pkt_ctx_set_staging(self._ctx, int(mode)), "pkt_ctx_set_staging")
 
     def set_walk(self, mode):
@@ -418,15 +418,31 @@ class PacketSlice:
         raise KeyError(name)
 
 
+def view(res, i):
+    """pkt_view (the C ABI's PacketSlice of packet i) over host (numpy) chain columns:
+    (status, [(hdr_type, offset)], payload_off, payload_len); no headers unless status is OK."""
+    from . import _lib
+    L = _lib.load()
+    need = ("status", "n_hdrs", "hdr_type", "hdr_off", "payload_off", "payload_len")
+    cols = {c: np.ascontiguousarray(res[c]) for c in need}
+    n = cols["status"].shape[0]
+    o = _lib.PktOut()
+    for c in need:
+        setattr(o, c, cols[c].ctypes.data)
+    ty, of = (ctypes.c_uint8 * MAX_HDRS)(), (ctypes.c_uint16 * MAX_HDRS)()
+    nh, po, pl = ctypes.c_uint32(), ctypes.c_uint16(), ctypes.c_uint16()
+    rc = L.pkt_view(ctypes.byref(o), n, int(i), ty, of, ctypes.byref(nh), ctypes.byref(po), ctypes.byref(pl))
+    if rc < 0:
+        raise ValueError(f"pkt_view({i}) failed ({rc})")
+    return rc, [(ty[k], of[k]) for k in range(nh.value)], po.value, pl.value
+
+
 def packet_slice(res, i, pkt):
-    """Build the PacketSlice of packet i from host (numpy) result columns and its bytes."""
-    if int(res["status"][i]) != OK:
-        raise ValueError(f"packet {i}: {STATUS_NAMES[int(res['status'][i])]} (the reference panics)")
+    """Build the PacketSlice of packet i from host (numpy) result columns and its bytes, through
+    pkt_view (the same per-packet view a Rust caller builds its PacketSlice from)."""
+    st, hl, po, pl = view(res, i)
+    if st != OK:
+        raise ValueError(f"packet {i}: {STATUS_NAMES[st]} (the reference panics)")
     pkt = bytes(pkt)
-    hdrs = []
-    for j in range(int(res["n_hdrs"][i])):
-        t = int(res["hdr_type"][j, i])
-        o = int(res["hdr_off"][j, i])
-        hdrs.append(HeaderSlice(t, memoryview(pkt)[o:]))
-    po, pl = int(res["payload_off"][i]), int(res["payload_len"][i])
+    hdrs = [HeaderSlice(t, memoryview(pkt)[o:]) for t, o in hl]
     return PacketSlice(hdrs, pkt[po:po + pl])

@@ -37,6 +37,11 @@ class PktFieldSpec(ctypes.Structure):
                 ("reserved", ctypes.c_uint16)]
 
 
+class PktGatherPiece(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_uint64), ("dst", ctypes.c_uint64), ("bytes", ctypes.c_uint64),
+                ("shard", ctypes.c_int32), ("reserved", ctypes.c_uint32)]
+
+
 class PktGenField(ctypes.Structure):
     _fields_ = [("field", PktFieldSpec), ("kind", ctypes.c_uint32), ("reserved", ctypes.c_uint32),
                 ("base", ctypes.c_uint64), ("step", ctypes.c_uint64), ("count", ctypes.c_uint64)]
@@ -104,6 +109,16 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_int)]),
     "pkt_chain_max_hdrs": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint32), _P]),
     "pkt_out_mask": (ctypes.c_uint64, [ctypes.POINTER(PktOut)]),
+    "pkt_view": (ctypes.c_int, [ctypes.POINTER(PktOut), ctypes.c_uint64, ctypes.c_uint64,
+                                ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint16),
+                                ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint16),
+                                ctypes.POINTER(ctypes.c_uint16)]),
+    "pkt_sizeof_gather_piece": (ctypes.c_size_t, []),
+    "pkt_gather_plan": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint32), ctypes.c_int,
+                                       ctypes.POINTER(PktGatherPiece), ctypes.c_uint64,
+                                       ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_mgpu_set_root_copy": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_mgpu_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
@@ -144,7 +159,8 @@ def load():
         raise ImportError("libpktgpu ABI version mismatch")
     if L.pkt_sizeof_out() != ctypes.sizeof(PktOut) or L.pkt_sizeof_batch() != ctypes.sizeof(PktBatch) \
             or L.pkt_sizeof_field_spec() != ctypes.sizeof(PktFieldSpec) \
-            or L.pkt_sizeof_gen_field() != ctypes.sizeof(PktGenField):
+            or L.pkt_sizeof_gen_field() != ctypes.sizeof(PktGenField) \
+            or L.pkt_sizeof_gather_piece() != ctypes.sizeof(PktGatherPiece):
         raise ImportError("libpktgpu struct layout mismatch with pktgpu/_lib.py")
     _lib = L
     return L

@@ -65,6 +65,25 @@ def packed_pieces(columns, n, rows):
     return [po[k] for k in range(npc.value)], [pl[k] for k in range(npc.value)]
 
 
+def gather_plan(columns, ns, rows=None, merge=False):
+    """pkt_gather_plan: the messages of pkt_mgpu_parse_gather for shards of ns[i] packets with rows[i]
+    used slot rows -> ([(shard, src, dst, bytes)], recv_bytes).  Host only."""
+    from . import _lib
+    L = _lib.load()
+    nd = len(ns)
+    n_arr = (ctypes.c_uint64 * nd)(*[int(x) for x in ns])
+    r_arr = (ctypes.c_uint32 * nd)(*[int(x) for x in rows]) if rows is not None else None
+    cnt, rb = ctypes.c_uint64(), ctypes.c_uint64()
+    mask = schema.column_mask(resolve_columns(columns))
+    if L.pkt_gather_plan(mask, nd, n_arr, r_arr, int(bool(merge)), None, 0, ctypes.byref(cnt), ctypes.byref(rb)) != 0:
+        raise ValueError("pkt_gather_plan: bad arguments")
+    arr = (_lib.PktGatherPiece * max(1, cnt.value))()
+    if L.pkt_gather_plan(mask, nd, n_arr, r_arr, int(bool(merge)), arr, cnt.value, ctypes.byref(cnt),
+                         ctypes.byref(rb)) != 0:
+        raise ValueError("pkt_gather_plan: bad arguments")
+    return [(p.shard, p.src, p.dst, p.bytes) for p in arr[:cnt.value]], rb.value
+
+
 def shard_range(n, nshards, i):
     """The library's contiguous split (pkt_shard_range): [lo, hi) of shard i."""
     from . import _lib
@@ -114,6 +133,11 @@ class MultiParser:
 
     def ctx(self, i):
         return self._L.pkt_mgpu_ctx(self._mg, i)
+
+    def set_root_copy(self, enable):
+        """pkt_mgpu_set_root_copy: the root's own pieces by device copy (True, default) or by RCCL
+        send/recv to itself (False)."""
+        self._check(self._L.pkt_mgpu_set_root_copy(self._mg, int(bool(enable))), "pkt_mgpu_set_root_copy")
 
     def synchronize(self):
         self._check(self._L.pkt_mgpu_synchronize(self._mg), "pkt_mgpu_synchronize")
@@ -266,10 +290,7 @@ class MultiParser:
         return shard_out
 
     def recv_bytes(self, shards, columns, merge):
-        cols = resolve_columns(columns)
-        if merge:
-            return packed_bytes(cols, sum(s[1] for s in shards))
-        return sum((packed_bytes(cols, s[1]) + 255) // 256 * 256 for s in shards)
+        return gather_plan(columns, [s[1] for s in shards], None, merge)[1]
 
     def parse_gather(self, shards, entry="parse", columns="all", root=0, merge=False,
                      shard_out=None, recv=None):

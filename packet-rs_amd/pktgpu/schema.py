@@ -8,7 +8,7 @@ change without bumping PKTGPU_ABI_VERSION.
 import numpy as np
 
 MAX_HDRS = 16
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 # pkt_status_t
 OK, TRUNCATED, DEPTH_LIMIT = 0, 1, 2

@@ -17,9 +17,9 @@ C_SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": 
              "int": "c_int", "size_t": "usize", "char": "c_char", "void": "c_void",
              "pkt_ctx_t": "PktCtx", "pkt_batch_t": "PktBatch", "pkt_out_t": "PktOut", "pkt_chain_t": "PktChain",
              "pkt_field_spec_t": "PktFieldSpec", "pkt_gen_field_t": "PktGenField", "pkt_gen_t": "PktGen",
-             "pkt_mgpu_t": "PktMgpu"}
+             "pkt_mgpu_t": "PktMgpu", "pkt_gather_piece_t": "PktGatherPiece"}
 STRUCTS = {"pkt_batch": "PktBatch", "pkt_out": "PktOut", "pkt_field_spec": "PktFieldSpec", "pkt_chain": "PktChain",
-           "pkt_gen_field": "PktGenField"}
+           "pkt_gen_field": "PktGenField", "pkt_gather_piece": "PktGatherPiece"}
 
 
 def _strip(src):
@@ -95,7 +95,7 @@ def header_functions():
 
 def generate():
     st, fn = header_structs(), header_functions()
-    lines = ["// src/gpu.rs — packet_rs's batched GPU decode through libpktgpu (include/pktgpu.h, ABI v4).",
+    lines = ["// src/gpu.rs — packet_rs's batched GPU decode through libpktgpu (include/pktgpu.h, ABI v5).",
              "// Every struct and function of the header, field for field (tests/test_rust_binding.py).",
              "#![allow(non_camel_case_types, dead_code)]",
              "use std::os::raw::{c_char, c_int, c_void};", ""]

@@ -41,15 +41,15 @@ def test_line_bytes_indexed_vs_brute_force():
 
 
 def test_gpus_beyond_visible_devices_exits_nonzero():
-    """`bench.py --gpus N` with fewer visible devices must fail, in both forms (the
-    pkt_mgpu one-process form and the --per-rank launcher).  This container has no GPU."""
+    """`bench.py --gpus N` with fewer visible devices must fail.  This container has
+    no GPU."""
     import subprocess
     import sys
     import pytest
     torch = pytest.importorskip("torch")
     if torch.cuda.device_count() >= 2:
         pytest.skip("two or more devices visible")
-    for extra in ([], ["--per-rank"]):
+    for extra in ([],):
         r = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2",
                             "--warmup", "1", "--no-cpu-baseline"] + extra,
                            capture_output=True, text=True, timeout=300,

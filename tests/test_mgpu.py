@@ -95,6 +95,101 @@ def test_shard_range_matches_dist():
     assert L.pkt_shard_range(10, 2, 2, ctypes.byref(lo), ctypes.byref(hi)) != 0
 
 
+def _packed_offsets(L, mask, n):
+    """{column: byte offset} of an n-packet packed buffer (pkt_out_packed) and its size."""
+    o = _lib.PktOut()
+    nb = ctypes.c_uint64()
+    base = 1 << 40
+    assert L.pkt_out_packed(mask, n, ctypes.c_void_p(base), ctypes.byref(o), ctypes.byref(nb)) == 0
+    return {c: getattr(o, c) - base for c in schema.COLUMN_NAMES if getattr(o, c)}, nb.value
+
+
+def _pack(L, cols, res, lo, hi):
+    """Packets [lo, hi) of an oracle result as the shard's packed buffer (bytes)."""
+    mask = schema.column_mask(cols)
+    n = hi - lo
+    off, nb = _packed_offsets(L, mask, n)
+    buf = np.full(max(nb, 1), 0xEE, np.uint8)  # poison: bytes the plan must not rely on
+    for c in cols:
+        v = res[c][:, lo:hi] if c in ("hdr_type", "hdr_off") else res[c][lo:hi]
+        b = np.ascontiguousarray(v).view(np.uint8).reshape(-1)
+        buf[off[c]:off[c] + b.size] = b
+    return buf
+
+
+def _unpack(L, cols, buf, base, n):
+    mask = schema.column_mask(cols)
+    off, _ = _packed_offsets(L, mask, n)
+    out = {}
+    for c in cols:
+        dt = schema.column_dtype(c)
+        shp = schema.column_shape(c, n)
+        nbytes = int(np.prod(shp)) * dt.itemsize
+        out[c] = buf[base + off[c]:base + off[c] + nbytes].view(dt).reshape(shp)
+    return out
+
+
+@pytest.mark.parametrize("nd", [2, 3, 8])
+@pytest.mark.parametrize("merge", [False, True])
+@pytest.mark.parametrize("cfg", ["c2", "c4"])
+def test_gather_plan_executed_on_host(nd, merge, cfg):
+    """pkt_mgpu_parse_gather's message plan (pkt_gather_plan, the same function the
+    device gather issues) executed with host memcpy over oracle-parsed packed shards of uneven size
+    (an empty shard among them): the root buffer must hold exactly the whole batch's oracle output
+    (merge = 1), or each shard's tuples at its 256-B aligned block (merge = 0) — sharding is legal
+    because fast::parse is pure per packet (reference src/parser/fast.rs:5-12)."""
+    from pktgpu import mgpu
+    L = _L()
+    rng = np.random.default_rng(nd * 7 + merge + (cfg == "c4"))
+    cuts = sorted(int(x) for x in rng.integers(0, 4000, nd - 1))
+    if nd >= 3:
+        cuts[1] = cuts[0]  # an empty shard
+    bounds = [0] + cuts + [4000 + nd]
+    n = bounds[-1]
+    if cfg == "c2":
+        slab = gen.gen_c2(n, seed=nd)
+        cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+        res = oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8)
+    else:
+        buf, offs, lens = gen.gen_c4(n, seed=nd)
+        cols = list(schema.COLUMN_NAMES)
+        res = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    ns = [bounds[i + 1] - bounds[i] for i in range(nd)]
+    rows = [int(res["n_hdrs"][bounds[i]:bounds[i + 1]].max()) if ns[i] else 0 for i in range(nd)]
+    shards = [_pack(L, cols, res, bounds[i], bounds[i + 1]) for i in range(nd)]
+    plan, rb = mgpu.gather_plan(cols, ns, rows, merge)
+    recv = np.full(rb, 0xCD, np.uint8)
+    for shard, src, dst, nbytes in plan:
+        assert ns[shard] and src + nbytes <= shards[shard].size and dst + nbytes <= rb
+        recv[dst:dst + nbytes] = shards[shard][src:src + nbytes]
+    if merge:
+        _compare(_unpack(L, cols, recv, 0, n), res, f"{cfg} nd={nd} merged")
+    else:
+        o = 0
+        for i in range(nd):
+            if ns[i]:
+                sub = {k: (v[:, bounds[i]:bounds[i + 1]] if k in ("hdr_type", "hdr_off") else v[bounds[i]:bounds[i + 1]])
+                       for k, v in res.items()}
+                _compare(_unpack(L, cols, recv, o, ns[i]), sub, f"{cfg} nd={nd} shard {i}")
+            o += (_packed_offsets(L, schema.column_mask(cols), ns[i])[1] + 255) // 256 * 256
+    # rows = None moves all 16 slot rows; the plan's receive size is independent of rows
+    plan16, rb16 = mgpu.gather_plan(cols, ns, None, merge)
+    assert rb16 == rb and sum(p[3] for p in plan16) >= sum(p[3] for p in plan)
+
+
+def test_gather_plan_rejects_bad_arguments():
+    L = _L()
+    n = (ctypes.c_uint64 * 2)(5, 6)
+    cnt, rb = ctypes.c_uint64(), ctypes.c_uint64()
+    assert L.pkt_gather_plan(1 << 49, 2, n, None, 0, None, 0, ctypes.byref(cnt), ctypes.byref(rb)) != 0
+    assert L.pkt_gather_plan(3, 0, n, None, 0, None, 0, ctypes.byref(cnt), ctypes.byref(rb)) != 0
+    assert L.pkt_gather_plan(3, 2, n, None, 2, None, 0, ctypes.byref(cnt), ctypes.byref(rb)) != 0
+    bad_rows = (ctypes.c_uint32 * 2)(3, 17)
+    assert L.pkt_gather_plan(3, 2, n, bad_rows, 0, None, 0, ctypes.byref(cnt), ctypes.byref(rb)) != 0
+    assert L.pkt_gather_plan(3, 2, n, None, 0, None, 5, ctypes.byref(cnt), ctypes.byref(rb)) != 0
+    assert L.pkt_sizeof_gather_piece() == ctypes.sizeof(_lib.PktGatherPiece) == 32
+
+
 def test_mgpu_create_rejects_bad_device_lists():
     L = _L()
     h = ctypes.c_void_p()
@@ -226,3 +321,76 @@ def test_bench_mgpu_leg_at_one_device():
     g = line["c5"]["gather"]
     assert g["slot_rows_moved"] == 3
     assert 69 <= g["bytes_per_pkt_moved"] <= 70, g
+    assert g["bytes_into_root"] > 0 and g["rccl_messages"] >= 2, g  # RCCL moved the root's own shard
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("merge", [False, True])
+@pytest.mark.parametrize("cfg", ["c2", "c4"])
+def test_mgpu_parse_gather_rccl_root_self_send(MP, merge, cfg):
+    """with pkt_mgpu_set_root_copy(0) the root's own pieces go through RCCL
+    (ncclSend / ncclRecv to itself inside the group), so on a 1-GPU box the gather still executes
+    RCCL transfers; the result must equal the oracle over the whole batch."""
+    MP.set_root_copy(False)
+    try:
+        if cfg == "c2":
+            n = 65_537
+            slab = gen.gen_c2(n, seed=78)
+            cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+            shards = MP.shard_fixed(slab, n, 64)
+            o = oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8)
+        else:
+            n = 30_011
+            buf, offs, lens = gen.gen_c4(n, seed=79)
+            cols = list(schema.COLUMN_NAMES)
+            shards = MP.shard_indexed(buf, offs, lens)
+            o = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+        for rep in range(2):
+            views, recv, _ = MP.parse_gather(shards, columns=cols, merge=merge)
+            MP.synchronize()
+            if merge:
+                _compare(views, o, f"{cfg} merged rccl-self rep {rep}")
+            else:
+                merged = {c: np.concatenate([v[c].cpu().numpy() for v in views if v],
+                                            axis=1 if c in ("hdr_type", "hdr_off") else 0) for c in cols}
+                _compare(merged, o, f"{cfg} per-shard rccl-self rep {rep}")
+    finally:
+        MP.set_root_copy(True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("streams", [1, 4])
+def test_mgpu_parse_steps_vs_oracle(MP, streams):
+    """pkt_mgpu_parse_steps (the bench's timed entry) with several steps of distinct
+    inputs and outputs, round-robin over 1 or 4 streams, one step with n = 0 and no output: after
+    synchronize() every step's packed output equals the oracle's parse of its own input."""
+    import torch
+    from pktgpu.mgpu import packed_bytes, packed_views
+    nd = MP.ndev
+    cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+    steps, refs = [], []
+    for k in range(7):
+        per_dev, ref_dev = [], []
+        for i, d in enumerate(MP.torch_devices):
+            n = 0 if k == 3 else 4096 * (k + 1) + 17 * i
+            slab = gen.gen_c2(max(n, 1), seed=1000 + 10 * k + i) if n else np.zeros(64, np.uint8)
+            t = torch.from_numpy(slab.reshape(-1)).to(d)
+            out = torch.full((max(1, packed_bytes(cols, n)),), 0xEE, dtype=torch.uint8, device=d)
+            per_dev.append(((t, n, 64, None, None), out))
+            ref_dev.append((slab, n))
+        steps.append(per_dev)
+        refs.append(ref_dev)
+    plan = MP.steps_plan(steps)
+    b, o, _ = plan
+    for i in range(nd):
+        o[3 * nd + i] = None  # the empty step has no output buffer
+    torch.cuda.synchronize()
+    MP.parse_steps(plan, "parse", cols, streams=streams)
+    MP.synchronize()
+    for k in range(7):
+        for i in range(nd):
+            slab, n = refs[k][i]
+            if not n:
+                continue
+            got = {c: v.cpu().numpy() for c, v in packed_views(steps[k][i][1], cols, n).items()}
+            _compare(got, oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8), f"step {k} dev {i}")

@@ -144,3 +144,25 @@ def test_device_index_then_parse(P):
             assert not (valid & (gv != ov)).any(), k
         else:
             assert np.array_equal(gv, ov), k
+
+
+def test_one_ctx_growing_and_shrinking_captures():
+    """one ctx indexes captures whose region count grows within the scratch
+    buffer's slack and shrinks again, over many epochs.  The scan-block states must never sit on an
+    earlier call's per-region words (file positions / prefixes that can look 'published' in the
+    current epoch): the scratch layout is fixed by the allocated capacity, not by each call's K."""
+    import pktgpu
+    P2 = pktgpu.Parser(0)  # a fresh ctx: its scratch is first sized by the smallest capture
+    try:
+        caps = {}
+        for n in (200, 5400, 6600, 200, 7000, 5800, 40, 8000):  # ~9 to ~360 4-KiB regions
+            caps[n] = gen.gen_c4(n, seed=900 + n)
+        order = [200, 5400, 6600, 200, 7000, 5800, 40, 8000] * 5
+        for rep, n in enumerate(order):
+            buf, offs, lens = caps[n]
+            o, l, m = P2.pcap_index(dev(buf))
+            assert m == n, (rep, n, m)
+            assert np.array_equal(o.cpu().numpy(), offs), (rep, n)
+            assert np.array_equal(l.cpu().numpy(), lens), (rep, n)
+    finally:
+        P2.close()

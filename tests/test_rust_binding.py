@@ -51,3 +51,26 @@ def test_c_type_mapping():
     assert rb.rust_of(*rb.c_type("uint64_t off[2]")) == "*mut u64"
     assert rb.rust_of(*rb.c_type("const char **name")) == "*mut *const c_char"
     assert rb.rust_of(*rb.c_type("uint32_t stride")) == "u32"
+
+
+def test_packet_slice_adapter_builds_every_reference_slice_type():
+    """the adapter `slices()` in INTEGRATION.md turns pkt_view's (type, offset) list into
+    the reference's own PacketSlice (lib.rs:136-140) with `<Hdr>Slice::from(&arr[o..o + <Hdr>::size()])`
+    + insert + set_payload (packet.rs:714-731).  Its match arms must map every header id of pktgpu.h to
+    the Slice type of the make_header! invocation with that name (tests/golden/make_header_names.json,
+    transcribed from headers.rs:529-827), and the adapter must call pkt_view."""
+    import json
+    sys.path.insert(0, os.path.join(REPO, "packet-rs_amd"))
+    from pktgpu import schema
+    code = _rust_code()
+    body = code[code.index("pub fn slices<'a>"):]
+    assert "pkt_view(" in body and "set_payload(" in body and "PacketSlice::new()" in body
+    arms = re.findall(r"(\d+) => s\.insert\((\w+)Slice::from\(&arr\[o\.\.o \+ (\w+)::size\(\)\]\)\)", body)
+    gold = [h["name"] for h in json.load(open(os.path.join(REPO, "tests", "golden", "make_header_names.json")))["headers"]]
+    assert len(gold) == 21 and len(arms) == len(gold)
+    for tid, slice_name, size_name in arms:
+        t = int(tid)
+        assert slice_name == size_name == schema.HDR_NAMES[t], (t, slice_name, size_name)
+    assert [a[1] for a in arms] == gold
+    # the list is inserted back to front (insert puts a header at position 0)
+    assert "for k in (0..nh as usize).rev()" in body
