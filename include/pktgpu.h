@@ -279,6 +279,15 @@ int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
 int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
                     const pkt_out_t *out, void *stream);
 
+/* `nbatch` independent batches: batches[k] -> outs[k], as nbatch pkt_parse_batch calls would write
+ * them.  When the batches have the same n (<= 2^26), stride and layout (indexed or not, lens or not),
+ * nbatch <= 16, and every batch's column pointers lie at one common byte distance from batch 0's (one
+ * packed output buffer per batch, pkt_out_packed, qualifies), it is ONE launch whose grid covers every
+ * batch's tiles, so the launch's ramp and drain are paid once; otherwise one launch per batch.
+ * Asynchronous on `stream`. */
+int pkt_parse_batches(pkt_ctx_t *ctx, const pkt_batch_t *batches, uint32_t nbatch, int entry,
+                      const pkt_out_t *outs, void *stream);
+
 /* ---- host-memory path ----
  * The reference's path starts and ends in host memory (a pcap file, a NIC ring).  One call moves
  * a HOST batch through the device: `batch` (slab, offsets, lens) and `out` (column pointers, the
@@ -292,6 +301,17 @@ int pkt_parse_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry,
  * One host call at a time per ctx. */
 int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pkt_out_t *out,
                    uint64_t chunk);
+/* The capture path of tests/pcap.rs:7-37 end to end, host memory in and out: a pcap file in HOST
+ * memory (`buf`, `len` bytes; pinned from pkt_host_alloc for the full link rate) is copied to the
+ * device once, indexed there (pkt_pcap_index_device: same records, count, cap behaviour and errors
+ * as pkt_pcap_index) and parsed with `entry` (an indexed batch over the file in place); the requested
+ * columns of `out` are HOST memory sized for `cap` records, slot columns strided by cap
+ * ([PKT_MAX_HDRS][cap]).  Pinned columns are written by the parse kernel over the link directly; others
+ * through the staged pipeline of pkt_parse_host.  offsets / lens (HOST, [cap], may be NULL) receive
+ * the records' (data offset, incl_len).  *n_out = the record count (> cap: only the first cap are
+ * parsed).  Blocking.  One host call at a time per ctx. */
+int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
+                        uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out);
 /* Pinned (page-locked) host memory for pkt_parse_host buffers. */
 int pkt_host_alloc(pkt_ctx_t *ctx, uint64_t bytes, void **p);
 int pkt_host_free(pkt_ctx_t *ctx, void *p);

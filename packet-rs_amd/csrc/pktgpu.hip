@@ -223,7 +223,7 @@ __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uin
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-// Diagnostic build only (-DPKTGPU_STAMPS=1, scripts/gpu_stamps.sh): s_memtime stamps per wave of the
+// Diagnostic build only (-DPKTGPU_STAMPS=1: scripts/build_variant.sh, read by scripts/stamps.py): s_memtime stamps per wave of the
 // parse kernel — start, windows in LDS, walk done, emit issued, stores drained — plus the wave's
 // hardware id, written by lane 0 to a debug buffer no other code reads (pkt_debug_stamps).  In the
 // normal build no stamp executes.
@@ -305,14 +305,11 @@ __device__ __forceinline__ const DispatchLds* tables(uint8_t* lds, size_t at, ui
 // windows (25.6 KB per block, 6 blocks per CU), 4 for the 144-byte ones (37.9 KB, 4 blocks); wider
 // windows unconstrained.
 __host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : 6) : 8); }
+// Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
 template <int NCH, uint32_t GM, int WK>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
-void parse_kernel(KParams p) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
-    PKT_STAMP(0);
-    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
-    const uint32_t base = blockIdx.x * (uint32_t)kBlock;  // within this launch
+__device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
+                                            uint64_t* pkt_st) {
+    const uint32_t base = blk * (uint32_t)kBlock;  // within this launch
     const bool act = base + threadIdx.x < p.n;
     u32x4 chunk[NCH];
     uint64_t off;
@@ -360,6 +357,57 @@ void parse_kernel(KParams p) {
     }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
     parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act, pkt_st, T);
+}
+
+template <int NCH, uint32_t GM, int WK>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
+void parse_kernel(KParams p) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
+    PKT_STAMP(0);
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
+    parse_block<NCH, GM, WK>(p, blockIdx.x, lds, T, pkt_st);
+}
+
+// ---- several batches in one launch (pkt_parse_batches) ----
+// K batches of the same size and layout whose outputs lie at one common byte distance from batch
+// 0's (e.g. one packed output buffer each): block j parses tile j % bpb of batch j / bpb.  Every
+// per-batch value comes from the kernel arguments (a scalar load at a computed offset: no table
+// read from memory before the block can start), and the launch's ramp and drain are paid once for
+// the K batches instead of once per batch.
+constexpr int kMaxMulti = 16;
+struct MultiBatch {
+    const uint8_t* slab;
+    uint64_t slab_len;
+    const uint64_t* offsets;
+    const uint32_t* lens;
+    int64_t out_delta;  // bytes from batch 0's column pointers to this batch's
+};
+struct MultiParams {
+    KParams base;  // batch 0 (its slab, index, outputs), the shared n / stride / entry / knobs
+    uint32_t bpb;  // blocks per batch
+    uint32_t k;
+    MultiBatch per[kMaxMulti];
+};
+
+template <int NCH, uint32_t GM, int WK>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
+void parse_multi_kernel(MultiParams mp) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+    uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
+    const uint32_t b = blockIdx.x / mp.bpb;  // wave-uniform
+    const MultiBatch& mb = mp.per[b];
+    KParams p = mp.base;
+    p.slab = mb.slab;
+    p.slab_len = mb.slab_len;
+    p.offsets = mb.offsets;
+    p.lens = mb.lens;
+    uint8_t** col = reinterpret_cast<uint8_t**>(&p.out);
+#pragma unroll
+    for (int c = 0; c < 49; c++)
+        if (col[c]) col[c] += mb.out_delta;
+    parse_block<NCH, GM, WK>(p, blockIdx.x - b * mp.bpb, lds, T, pkt_st);
 }
 
 template <int NCH, uint32_t GM, int WK, bool STAGED>
@@ -569,7 +617,12 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
 enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
 
 template <int NCH, uint32_t GM, int WK>
-hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
+hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiParams* mp) {
+    if (mp) {  // several batches, one launch (windows only)
+        hipLaunchKernelGGL((parse_multi_kernel<NCH, GM, WK>), dim3(mp->bpb * mp->k), dim3(kBlock),
+                           with_tables(window_lds(NCH), WK), s, *mp);
+        return hipGetLastError();
+    }
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), with_tables(span_region(NCH), WK), s, kp);
@@ -584,23 +637,23 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s) {
 // Kernels are compiled per fully-requested column-group set; the lockstep walk (mixed traffic)
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
-hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s) {
+hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s, const MultiParams* mp) {
     // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 9 and
     // 17 chunks only (parse_impl widens a narrower request)
     if constexpr (NCH >= 6) if (wk == 1) {
         switch (gm) {
-            case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s);
-            case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s);
-            default: return launch_mode<NCH, G_RUNTIME | G_NT, 1>(kp, mode, s);
+            case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp);
+            case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp);
+            default: return launch_mode<NCH, G_RUNTIME | G_NT, 1>(kp, mode, s, mp);
         }
     }
     switch (gm) {
-        case G_CHAIN: return launch_mode<NCH, G_CHAIN, 0>(kp, mode, s);
-        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP, 0>(kp, mode, s);
+        case G_CHAIN: return launch_mode<NCH, G_CHAIN, 0>(kp, mode, s, mp);
+        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP, 0>(kp, mode, s, mp);
         case G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP:
-            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP, 0>(kp, mode, s);
-        case G_ALL: return launch_mode<NCH, G_ALL, 0>(kp, mode, s);
-        default: return launch_mode<NCH, G_RUNTIME, 0>(kp, mode, s);
+            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP, 0>(kp, mode, s, mp);
+        case G_ALL: return launch_mode<NCH, G_ALL, 0>(kp, mode, s, mp);
+        default: return launch_mode<NCH, G_RUNTIME, 0>(kp, mode, s, mp);
     }
 }
 
@@ -777,6 +830,9 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
             (void)hipFree(ctx->hp.lens[k]);
             (void)hipFree(ctx->hp.out[k]);
         }
+        (void)hipFree(ctx->hp.file);
+        (void)hipFree(ctx->hp.ioffs);
+        (void)hipFree(ctx->hp.ilens);
     }
     delete ctx;
     return PKT_SUCCESS;
@@ -809,13 +865,53 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
 }
 
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max = nullptr);
+                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max = nullptr,
+                      uint64_t slot_stride = 0, MultiParams* mp = nullptr);
 
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
     // the kernel reads whole 16-byte chunks, clamped to the last one of the slab
     if (b && b->n && b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
     return parse_impl(ctx, b, entry, out, stream, 0, ctx ? ctx->staging : 0);
+}
+
+int pkt_parse_batches(pkt_ctx_t* ctx, const pkt_batch_t* batches, uint32_t nbatch, int entry, const pkt_out_t* outs,
+                      void* stream) {
+    if (!ctx || (nbatch && (!batches || !outs))) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    // One launch when the batches share size and layout and their outputs sit at one common byte
+    // distance from batch 0's (per column); otherwise one pkt_parse_batch each (same results).
+    bool one = nbatch >= 2 && nbatch <= (uint32_t)kMaxMulti && ctx->staging != 2;
+    const pkt_batch_t& b0 = batches[0];
+    const void* const* c0 = nbatch ? reinterpret_cast<const void* const*>(&outs[0]) : nullptr;
+    MultiParams mp;
+    for (uint32_t k = 0; k < nbatch && one; k++) {
+        const pkt_batch_t& b = batches[k];
+        one = b.n == b0.n && b.n > 0 && b.n <= kLaunchChunk && b.stride == b0.stride &&
+              (b.offsets == nullptr) == (b0.offsets == nullptr) && (b.lens == nullptr) == (b0.lens == nullptr) &&
+              b.slab && ((uintptr_t)b.slab & 15) == 0 && b.slab_len >= 16;
+        const void* const* ck = reinterpret_cast<const void* const*>(&outs[k]);
+        int64_t delta = 0;
+        bool have = false;
+        for (int c = 0; c < 49 && one; c++) {
+            if ((ck[c] == nullptr) != (c0[c] == nullptr)) one = false;
+            if (!ck[c]) continue;
+            const int64_t d = (int64_t)((uintptr_t)ck[c] - (uintptr_t)c0[c]);
+            if (have && d != delta) one = false;
+            delta = d;
+            have = true;
+        }
+        if (one) mp.per[k] = MultiBatch{b.slab, b.slab_len, b.offsets, b.lens, delta};
+    }
+    if (!one) {
+        for (uint32_t k = 0; k < nbatch; k++) {
+            const int rc = pkt_parse_batch(ctx, &batches[k], entry, &outs[k], stream);
+            if (rc != PKT_SUCCESS) return rc;
+        }
+        return PKT_SUCCESS;
+    }
+    mp.k = nbatch;
+    mp.bpb = (uint32_t)((b0.n + kBlock - 1) / kBlock);
+    return parse_impl(ctx, &b0, entry, &outs[0], stream, 0, ctx->staging, nullptr, 0, &mp);
 }
 
 }  // extern "C"
@@ -845,7 +941,8 @@ extern "C" {
 
 // `staging` = the ctx's knob, or the host path's override (wave spans over the link).
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
-                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max) {
+                      void* stream, uint64_t off_bias, int staging, uint32_t* nh_max, uint64_t slot_stride,
+                      MultiParams* mp) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -893,7 +990,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         kp.lens = adv(b->lens, i0);
         kp.off_bias = off_bias;
         kp.i0 = i0;
-        kp.n_slot_stride = b->n;
+        kp.n_slot_stride = slot_stride ? slot_stride : b->n;  // the slot columns' row stride
         kp.stride = b->stride;
         kp.n = (uint32_t)cnt;
         kp.entry = entry;
@@ -904,13 +1001,15 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
+        if (mp) mp->base = kp;  // batch 0 of a multi-batch launch (n <= kLaunchChunk: one chunk)
+        const int md = mp ? M_TILE : mode;
         // compiled window widths (chunks): a request between two is served by the wider one
-        if (nch <= 2) e = launch_gm<2>(kp, gm, mode, wk, s);
-        else if (nch <= 4) e = launch_gm<4>(kp, gm, mode, wk, s);
-        else if (nch <= 5) e = launch_gm<5>(kp, gm, mode, wk, s);
-        else if (nch <= 6) e = launch_gm<6>(kp, gm, mode, wk, s);
-        else if (nch <= 9) e = launch_gm<9>(kp, gm, mode, wk, s);
-        else e = launch_gm<17>(kp, gm, mode, wk, s);
+        if (nch <= 2) e = launch_gm<2>(kp, gm, md, wk, s, mp);
+        else if (nch <= 4) e = launch_gm<4>(kp, gm, md, wk, s, mp);
+        else if (nch <= 5) e = launch_gm<5>(kp, gm, md, wk, s, mp);
+        else if (nch <= 6) e = launch_gm<6>(kp, gm, md, wk, s, mp);
+        else if (nch <= 9) e = launch_gm<9>(kp, gm, md, wk, s, mp);
+        else e = launch_gm<17>(kp, gm, md, wk, s, mp);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;
@@ -930,45 +1029,16 @@ int pkt_host_free(pkt_ctx_t* ctx, void* p) {
     return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipHostFree");
 }
 
-int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, uint64_t chunk) {
-    if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
-    if (b->n == 0) return PKT_SUCCESS;
-    if (!b->slab || b->slab_len == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "null or empty slab");
-    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
-    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
-    hipError_t e = hipSetDevice(ctx->device);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+// The staged host pipeline: the batch cut into chunks of `cn` packets over the ctx's three streams,
+// each chunk parsed into a device output slot and its columns copied to the host rows (the slot rows
+// once the chunk's n_hdrs maximum, reduced inside its parse, is known — one chunk later, so the host
+// never waits on the chunk it has just queued).  dev_in = false: `b` is host memory and each chunk's
+// bytes (+ offsets / lens) are copied in first; dev_in = true: `b` is already in device memory.
+static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, uint64_t chunk,
+                        bool dev_in, uint64_t slot_stride = 0) {
     HostPipe& hp = ctx->hp;
-    if (!hp.init) {
-        for (int k = 0; k < HostPipe::kSlots; k++) {
-            e = hipStreamCreateWithFlags(&hp.s[k], hipStreamNonBlocking);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&hp.ev[k], hipEventDisableTiming);
-            if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamCreate");
-        }
-        hp.init = true;
-    }
-    // Zero copy: when the slab, the index arrays and every requested column are pinned host memory
-    // mapped into the device (pkt_host_alloc), the kernel reads and writes them over PCIe directly —
-    // one launch, no staging copies, both link directions busy at once (DESIGN.md §7).
-    {
-        pkt_batch_t db = *b;
-        pkt_out_t dout = *out;
-        bool mapped = host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
-                      (!b->lens || host_mapped(b->lens, db.lens));
-        uint8_t** dc = reinterpret_cast<uint8_t**>(&dout);
-        for (int c = 0; c < 49 && mapped; c++)
-            if (dc[c]) mapped = host_mapped(dc[c], dc[c]);
-        if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
-            // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
-            // for a deep header (per-lane windows would, one dependent PCIe read each)
-            int rc = parse_impl(ctx, &db, entry, &dout, hp.s[0], 0, ctx->staging == 0 ? 2 : ctx->staging);
-            if (rc != PKT_SUCCESS) return rc;
-            e = hipStreamSynchronize(hp.s[0]);
-            return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipStreamSynchronize");
-        }
-    }
-    const uint64_t n = b->n;
+    hipError_t e = hipSuccess;
+    const uint64_t n = b->n, hstride = slot_stride ? slot_stride : n;  // host slot rows: [16][hstride]
     const uint64_t cn = std::min<uint64_t>(chunk ? chunk : (1ull << 18), n);
     const uint64_t nchunks = (n + cn - 1) / cn;
 
@@ -992,11 +1062,12 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         bytes = z > a ? z - a : 0;
     };
     uint64_t slab_need = 16;
-    for (uint64_t k = 0; k < nchunks; k++) {
-        uint64_t base, bytes;
-        span(k * cn, std::min(n, (k + 1) * cn), base, bytes);
-        slab_need = std::max(slab_need, bytes);
-    }
+    if (!dev_in)
+        for (uint64_t k = 0; k < nchunks; k++) {
+            uint64_t base, bytes;
+            span(k * cn, std::min(n, (k + 1) * cn), base, bytes);
+            slab_need = std::max(slab_need, bytes);
+        }
     // device output layout of one chunk: the requested columns, packed, 256-byte aligned
     const uint8_t* const* hcol = reinterpret_cast<const uint8_t* const*>(out);
     uint64_t col_off[49], out_need = 0;
@@ -1007,19 +1078,17 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         out_need += (rows * cn * kColSize[c] + 255) & ~(uint64_t)255;
     }
     for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
-    if ((e = grow(hp.slab, hp.slab_cap, (slab_need + 15) & ~(uint64_t)15)) != hipSuccess ||
+    if ((!dev_in && (e = grow(hp.slab, hp.slab_cap, (slab_need + 15) & ~(uint64_t)15)) != hipSuccess) ||
         (e = grow(hp.out, hp.out_cap, std::max<uint64_t>(out_need, 256))) != hipSuccess)
         return hip_fail(ctx, e, "hipMalloc (host pipeline)");
-    if (b->offsets || b->lens) {
+    if (!dev_in && (b->offsets || b->lens)) {
         uint64_t cap8 = hp.pkt_cap, cap4 = hp.pkt_cap;
         if ((e = grow(hp.offs, cap8, cn * 8)) != hipSuccess || (e = grow(hp.lens, cap4, cn * 8)) != hipSuccess)
             return hip_fail(ctx, e, "hipMalloc (host pipeline)");
         hp.pkt_cap = std::min(cap8, cap4);
     }
 
-    // Slot rows move only as far as each chunk's largest n_hdrs (when n_hdrs is requested): the
-    // chunk's count is reduced on the device after its parse and read on the host one chunk later,
-    // so the host waits for chunk k-1 only after chunk k is queued.
+    // Slot rows move only as far as each chunk's largest n_hdrs (when n_hdrs is requested)
     const bool slot_rows = (hcol[kColHdrType] || hcol[kColHdrOff]) && hcol[1] != nullptr;
     if (slot_rows && (e = ensure_max_scratch(ctx)) != hipSuccess) return hip_fail(ctx, e, "max scratch");
     auto copy_slots = [&](uint64_t kk) -> hipError_t {  // chunk kk's slot rows [0, R) to the host
@@ -1034,7 +1103,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         for (int c : {kColHdrType, kColHdrOff}) {
             if (!hcol[c] || !rows) continue;
             const uint64_t sz = kColSize[c];
-            hipError_t es = hipMemcpy2DAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, n * sz, hp.out[q] + col_off[c],
+            hipError_t es = hipMemcpy2DAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, hstride * sz, hp.out[q] + col_off[c],
                                              m * sz, m * sz, rows, hipMemcpyDeviceToHost, hp.s[q]);
             if (es != hipSuccess) return es;
         }
@@ -1045,30 +1114,50 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
         const int q = (int)(k % HostPipe::kSlots);
         hipStream_t s = hp.s[q];
         const uint64_t lo = k * cn, hi = std::min(n, lo + cn), m = hi - lo;
-        uint64_t base, bytes;
-        span(lo, hi, base, bytes);
-        // in: the chunk's bytes (+ offsets / lens)
-        if (bytes) e = hipMemcpyAsync(hp.slab[q], b->slab + base, bytes, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess && b->offsets)
-            e = hipMemcpyAsync(hp.offs[q], b->offsets + lo, m * 8, hipMemcpyHostToDevice, s);
-        if (e == hipSuccess && b->lens)
-            e = hipMemcpyAsync(hp.lens[q], b->lens + lo, m * 4, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) { rc = hip_fail(ctx, e, "hipMemcpyAsync H2D"); break; }
-        // parse: a chunk whose records cover no byte still parses (all TRUNCATED) against a
-        // 1-byte view; fixed-stride chunks index from the chunk's first packet
         pkt_batch_t db;
-        db.slab = hp.slab[q];
-        db.slab_len = std::max<uint64_t>(bytes, 1);
-        db.offsets = b->offsets ? hp.offs[q] : nullptr;
-        db.lens = b->lens ? hp.lens[q] : nullptr;
-        db.stride = b->stride;
-        db.reserved = 0;
-        db.n = m;
+        uint64_t bias = 0;
+        if (dev_in) {
+            db = *b;
+            if (b->offsets) {
+                db.offsets = b->offsets + lo;
+                db.lens = b->lens + lo;
+            } else {
+                const uint64_t a = std::min<uint64_t>(lo * (uint64_t)b->stride, b->slab_len);
+                db.slab = b->slab + a;  // 16-byte aligned: stride % 16 == 0 is checked by the caller
+                db.slab_len = std::max<uint64_t>(b->slab_len - a, 16);
+                if (b->lens) db.lens = b->lens + lo;
+            }
+            db.n = m;
+        } else {
+            uint64_t base, bytes;
+            span(lo, hi, base, bytes);
+            // in: the chunk's bytes (+ offsets / lens)
+            if (bytes) e = hipMemcpyAsync(hp.slab[q], b->slab + base, bytes, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && b->offsets)
+                e = hipMemcpyAsync(hp.offs[q], b->offsets + lo, m * 8, hipMemcpyHostToDevice, s);
+            if (e == hipSuccess && b->lens)
+                e = hipMemcpyAsync(hp.lens[q], b->lens + lo, m * 4, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) { rc = hip_fail(ctx, e, "hipMemcpyAsync H2D"); break; }
+            // a chunk whose records cover no byte still parses (all TRUNCATED) against a 1-byte view;
+            // fixed-stride chunks index from the chunk's first packet
+            db.slab = hp.slab[q];
+            db.slab_len = std::max<uint64_t>(bytes, 1);
+            db.offsets = b->offsets ? hp.offs[q] : nullptr;
+            db.lens = b->lens ? hp.lens[q] : nullptr;
+            db.stride = b->stride;
+            db.reserved = 0;
+            db.n = m;
+            bias = b->offsets ? base : 0;
+        }
         pkt_out_t dout;
         uint8_t** dcol = reinterpret_cast<uint8_t**>(&dout);
         for (int c = 0; c < 49; c++) dcol[c] = hcol[c] ? hp.out[q] + col_off[c] : nullptr;
         // (the device buffer always has >= 16 readable bytes, so a view shorter than 16 is safe)
-        rc = parse_impl(ctx, &db, entry, &dout, s, b->offsets ? base : 0, ctx->staging);
+        if (slot_rows && (e = hipMemsetAsync(ctx->mx.dev + q, 0, sizeof(uint32_t), s)) != hipSuccess) {
+            rc = hip_fail(ctx, e, "hipMemsetAsync");
+            break;
+        }
+        rc = parse_impl(ctx, &db, entry, &dout, s, bias, ctx->staging, slot_rows ? ctx->mx.dev + q : nullptr);
         if (rc != PKT_SUCCESS) break;
         // out: every requested per-packet column into its host rows [lo, hi); the slot rows of this
         // chunk once its count is known (after the next chunk is queued)
@@ -1078,7 +1167,7 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
             e = hipMemcpyAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, dcol[c], m * sz, hipMemcpyDeviceToHost, s);
         }
         if (e == hipSuccess && slot_rows) {
-            e = max_hdrs_async(ctx, dcol[1], m, q, s);
+            e = hipMemcpyAsync(ctx->mx.host + q, ctx->mx.dev + q, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipEventRecord(hp.ev[q], s);
         }
         if (e == hipSuccess && k > 0) e = copy_slots(k - 1);
@@ -1094,4 +1183,131 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     }
     return rc;
 }
+
+static int host_pipe_init(pkt_ctx_t* ctx) {
+    HostPipe& hp = ctx->hp;
+    if (hp.init) return PKT_SUCCESS;
+    for (int k = 0; k < HostPipe::kSlots; k++) {
+        hipError_t e = hipStreamCreateWithFlags(&hp.s[k], hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&hp.ev[k], hipEventDisableTiming);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipStreamCreate");
+    }
+    hp.init = true;
+    return PKT_SUCCESS;
+}
+
+// Are the requested columns of `out` all pinned host memory mapped into the device?  `dout` = the
+// same columns by their device addresses.
+static bool out_mapped(const pkt_out_t* out, pkt_out_t& dout) {
+    dout = *out;
+    uint8_t** dc = reinterpret_cast<uint8_t**>(&dout);
+    bool mapped = true;
+    for (int c = 0; c < 49 && mapped; c++)
+        if (dc[c]) mapped = host_mapped(dc[c], dc[c]);
+    return mapped;
+}
+
+int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, uint64_t chunk) {
+    if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    if (b->n == 0) return PKT_SUCCESS;
+    if (!b->slab || b->slab_len == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "null or empty slab");
+    if (b->offsets && !b->lens) return fail(ctx, PKT_ERR_INVALID_ARG, "offsets without lens");
+    if (!b->offsets && b->stride == 0) return fail(ctx, PKT_ERR_INVALID_ARG, "stride 0");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    int rc = host_pipe_init(ctx);
+    if (rc != PKT_SUCCESS) return rc;
+    HostPipe& hp = ctx->hp;
+    // Zero copy: when the slab, the index arrays and every requested column are pinned host memory
+    // mapped into the device (pkt_host_alloc), the kernel reads and writes them over PCIe directly —
+    // one launch, no staging copies, both link directions busy at once (DESIGN.md §7).
+    {
+        pkt_batch_t db = *b;
+        pkt_out_t dout;
+        const bool mapped = host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
+                            (!b->lens || host_mapped(b->lens, db.lens)) && out_mapped(out, dout);
+        if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
+            // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
+            // for a deep header (per-lane windows would, one dependent PCIe read each)
+            rc = parse_impl(ctx, &db, entry, &dout, hp.s[0], 0, ctx->staging == 0 ? 2 : ctx->staging);
+            if (rc != PKT_SUCCESS) return rc;
+            e = hipStreamSynchronize(hp.s[0]);
+            return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipStreamSynchronize");
+        }
+    }
+    return staged_parse(ctx, b, entry, out, chunk, false);
+}
+
+int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                        uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out) {
+    if (!ctx || !buf || !out || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    *n_out = 0;
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    int rc = host_pipe_init(ctx);
+    if (rc != PKT_SUCCESS) return rc;
+    HostPipe& hp = ctx->hp;
+    for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
+    // the file and its index on the device (grown on demand; +16: the kernels' readable tail)
+    const uint64_t fbytes = ((len + 15) & ~(uint64_t)15) + 16;
+    if (fbytes > hp.file_cap) {
+        (void)hipFree(hp.file);
+        hp.file = nullptr;
+        hp.file_cap = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&hp.file), fbytes + fbytes / 4)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMalloc (pcap file)");
+        hp.file_cap = fbytes + fbytes / 4;
+    }
+    if (cap > hp.idx_cap) {
+        (void)hipFree(hp.ioffs);
+        (void)hipFree(hp.ilens);
+        hp.ioffs = nullptr;
+        hp.ilens = nullptr;
+        hp.idx_cap = 0;
+        const uint64_t c2 = cap + cap / 4;
+        e = hipMalloc(reinterpret_cast<void**>(&hp.ioffs), c2 * 8);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&hp.ilens), c2 * 4);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
+        hp.idx_cap = c2;
+    }
+    hipStream_t s = hp.s[0];
+    // in: the whole file, one copy (the record chain is sequential: the index needs all of it)
+    if ((e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s)) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)");
+    uint64_t n = 0;
+    rc = pkt_pcap_index_device(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, &n, s);
+    if (rc != PKT_SUCCESS) return rc;
+    *n_out = n;
+    const uint64_t m = std::min(n, cap);
+    if (m == 0) return PKT_SUCCESS;
+    if (offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)");
+    if (lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)");
+    pkt_batch_t db;
+    db.slab = hp.file;
+    db.slab_len = len;
+    db.offsets = hp.ioffs;
+    db.lens = hp.ilens;
+    db.stride = 0;
+    db.reserved = 0;
+    db.n = m;
+    // out: pinned (mapped) columns are written by the parse kernel over the link directly; else the
+    // staged pipeline (device output slots, copies per chunk)
+    pkt_out_t dout;
+    if (out_mapped(out, dout)) {
+        rc = parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap);
+        if (rc != PKT_SUCCESS) return rc;
+        for (int k = 0; k < 2; k++)
+            if ((e = hipStreamSynchronize(hp.s[k])) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+        return PKT_SUCCESS;
+    }
+    rc = staged_parse(ctx, &db, entry, out, 0, true, cap);
+    if (rc != PKT_SUCCESS) return rc;
+    if ((e = hipStreamSynchronize(hp.s[1])) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+    return PKT_SUCCESS;
+}
+
 }  // extern "C"

@@ -19,6 +19,11 @@ struct HostPipe {
     uint32_t* lens[kSlots] = {};
     uint8_t* out[kSlots] = {};
     uint64_t slab_cap = 0, pkt_cap = 0, out_cap = 0;  // bytes per slot (pkt_cap: offs and lens)
+    // pkt_parse_pcap_host: the capture and its index on the device
+    uint8_t* file = nullptr;
+    uint64_t* ioffs = nullptr;
+    uint32_t* ilens = nullptr;
+    uint64_t file_cap = 0, idx_cap = 0;  // bytes; records
 };
 
 // Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.

@@ -204,6 +204,28 @@ class Parser:
                     "pkt_parse_host")
         return out
 
+    def parse_pcap_host(self, buf, cap, entry="parse", columns="all", out=None, index=True):
+        """pkt_parse_pcap_host: a pcap file in host memory (numpy uint8 / bytes; pinned via host_empty
+        for the full link rate) -> (n records, {column: numpy array} sized for `cap` records, slot
+        columns [16][cap], (offsets, lens) or None).  One blocking call: copy in, device index,
+        parse, columns out."""
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        a = np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else np.ascontiguousarray(buf, np.uint8)
+        if out is None:
+            out = {c: np.zeros(schema.column_shape(c, cap), schema.column_dtype(c)) for c in resolve_columns(columns)}
+        o = self._lib.PktOut()
+        for c, v in out.items():
+            setattr(o, c, v.ctypes.data if v.size else None)
+        offs = np.zeros(cap, np.uint64) if index else None
+        lens = np.zeros(cap, np.uint32) if index else None
+        n = ctypes.c_uint64()
+        self._check(self._L.pkt_parse_pcap_host(self._ctx, a.ctypes.data, a.size, e, ctypes.byref(o),
+                                                offs.ctypes.data if index else None,
+                                                lens.ctypes.data if index else None, int(cap), ctypes.byref(n)),
+                    "pkt_parse_pcap_host")
+        m = min(n.value, cap)
+        return n.value, out, ((offs[:m], lens[:m]) if index else None)
+
     def host_empty(self, shape, dtype):
         """A numpy array in pinned host memory (pkt_host_alloc), freed with the Parser."""
         dtype = np.dtype(dtype)
@@ -215,6 +237,34 @@ class Parser:
         self._pinned.append(p)
         buf = (ctypes.c_uint8 * max(1, nbytes)).from_address(p.value)
         return np.frombuffer(buf, dtype=np.uint8, count=nbytes).view(dtype).reshape(shape)
+
+    def parse_batches(self, batches, outs, entry="parse", stream=None):
+        """pkt_parse_batches: batches = [(slab, n, stride, offsets, lens)], outs = [{column: tensor}]
+        -> outs.  One launch over every batch when they share size and layout and their outputs lie
+        at one common distance (e.g. one packed buffer each, mgpu.packed_views); else one each."""
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        k = len(batches)
+        barr = (self._lib.PktBatch * max(1, k))()
+        oarr = (self._lib.PktOut * max(1, k))()
+        for i, (bt, out) in enumerate(zip(batches, outs)):
+            barr[i] = self._batch(*bt)
+            oarr[i] = self.out_struct(out)
+        self._check(self._L.pkt_parse_batches(self._ctx, barr, k, e, oarr, self._stream(stream)), "pkt_parse_batches")
+        return outs
+
+    def batches_call(self, batches, out_structs, entry=0, stream=None):
+        """A zero-argument callable issuing one prebuilt pkt_parse_batches (bench loop)."""
+        k = len(batches)
+        barr = (self._lib.PktBatch * k)(*batches)
+        oarr = (self._lib.PktOut * k)(*out_structs)
+        f, ctx, s = self._L.pkt_parse_batches, self._ctx, self._stream(stream)
+
+        def call():
+            rc = f(ctx, barr, k, entry, oarr, s)
+            if rc != 0:
+                self._check(rc, "pkt_parse_batches")
+        call.keep = (barr, oarr)
+        return call
 
     def launch(self, batch_struct, entry, out_struct, stream=None):
         """Relaunch with prebuilt ctypes structs (no per-call Python allocation; bench loop)."""

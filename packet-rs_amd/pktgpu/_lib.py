@@ -70,8 +70,12 @@ SIGNATURES = {
     "pkt_ctx_set_walk": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
+    "pkt_parse_batches": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_uint32, ctypes.c_int,
+                                         ctypes.POINTER(PktOut), _P]),
     "pkt_parse_host": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int, ctypes.POINTER(PktOut),
                                       ctypes.c_uint64]),
+    "pkt_parse_pcap_host": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut),
+                                           _P, _P, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_host_alloc": (ctypes.c_int, [_P, ctypes.c_uint64, ctypes.POINTER(_P)]),
     "pkt_host_free": (ctypes.c_int, [_P, _P]),
     "pkt_extract_fields": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.POINTER(PktChain),

@@ -714,3 +714,37 @@ def test_vlan_fastpath_boundaries(P, fast):
              label=f"vlan cols f{fast}")
     finally:
         P.set_fastpath(1)
+
+
+@pytest.mark.parametrize("same", [True, False])
+def test_parse_batches_vs_oracle(P, same):
+    """pkt_parse_batches — K = 3 batches in one call.  Equal sizes with one packed
+    output buffer each (a common column distance) take ONE launch over the three batches' tiles;
+    different sizes fall back to one launch per batch.  Every batch must equal the oracle."""
+    import torch
+    from pktgpu.mgpu import packed_bytes, packed_views
+    cols = schema.columns_of(["chain", "ether", "ipv4", "udp"])
+    sizes = [1 << 17] * 3 if same else [70001, 1, 130000]
+    bts, outs, refs = [], [], []
+    for k, n in enumerate(sizes):
+        slab = gen.gen_c2(n, seed=300 + k)
+        t = torch.from_numpy(slab.reshape(-1)).cuda()
+        buf = torch.full((packed_bytes(cols, n),), 0xEE, dtype=torch.uint8, device="cuda")
+        bts.append((t, n, 64, None, None))
+        outs.append(packed_views(buf, cols, n))
+        refs.append(oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8))
+    P.parse_batches(bts, outs)
+    for k in range(3):
+        compare({c: v.cpu().numpy() for c, v in outs[k].items()}, refs[k], f"batch {k} same={same}")
+    # indexed (C4) batches of equal size, all columns, one launch
+    bts, outs, refs = [], [], []
+    for k in range(3):
+        buf, offs, lens = gen.gen_c4(40000, seed=310 + k)
+        bts.append((torch.from_numpy(buf).cuda(), 40000, None, torch.from_numpy(offs).cuda(),
+                    torch.from_numpy(lens).cuda()))
+        b = torch.full((packed_bytes("all", 40000),), 0xEE, dtype=torch.uint8, device="cuda")
+        outs.append(packed_views(b, "all", 40000))
+        refs.append(oracle.parse_batch(buf, 40000, offsets=offs, lens=lens, nthreads=8))
+    P.parse_batches(bts, outs)
+    for k in range(3):
+        compare({c: v.cpu().numpy() for c, v in outs[k].items()}, refs[k], f"c4 batch {k}")

@@ -135,3 +135,40 @@ def test_pinned_async_parse_batch(P, staging):
     finally:
         P.set_staging(0)
     check(out, oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8), f"async staging={staging}")
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_pcap_host_end_to_end(P, pinned):
+    """pkt_parse_pcap_host — a capture in host memory (tests/pcap.rs:7-37 format) ->
+    device copy -> device index -> all-column parse -> host columns, one blocking call — equals the
+    host indexer + the oracle at 2^16 records; pinned columns take the kernel's direct writes over
+    the link, pageable ones the staged pipeline.  Slot columns are strided by cap."""
+    n = 1 << 16
+    buf, offs, lens = gen.gen_c4(n, seed=31)
+    cap = n + 123  # room to spare: the slot rows are strided by cap, not by the count
+    if pinned:
+        hb = P.host_empty((buf.size,), np.uint8)
+        hb[:] = buf
+        out = {c: P.host_empty(schema.column_shape(c, cap), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
+    else:
+        hb, out = buf, None
+    m, g, (o2, l2) = P.parse_pcap_host(hb, cap, out=out)
+    assert m == n
+    assert np.array_equal(o2, offs) and np.array_equal(l2, lens)
+    ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    got = {k: (v[:, :n] if k in ("hdr_type", "hdr_off") else v[:n]) for k, v in g.items()}
+    check(got, ref, f"pcap host pinned={pinned}")
+
+
+def test_pcap_host_cap_and_errors(P):
+    buf, offs, lens = gen.gen_c4(5000, seed=32)
+    m, g, (o2, l2) = P.parse_pcap_host(buf, 1234, columns=["chain", "ipv4"])
+    assert m == 5000 and np.array_equal(o2, offs[:1234]) and np.array_equal(l2, lens[:1234])
+    ref = oracle.parse_batch(buf, 1234, offsets=offs[:1234], lens=lens[:1234], columns=list(g), nthreads=8)
+    check(g, ref, "cap < count")
+    pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+    for bad in (pc[:-3], b"\x00" * 40):
+        with pytest.raises(RuntimeError):
+            P.parse_pcap_host(bad, 64)
+    m, g, _ = P.parse_pcap_host(pc, 22, columns=["chain"])
+    assert m == 22 and int(g["status"].max()) == 0
