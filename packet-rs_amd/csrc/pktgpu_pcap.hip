@@ -172,6 +172,24 @@ __device__ __forceinline__ int chain_local(const uint32_t* lw, uint32_t c, uint3
     return 1;
 }
 
+// chain_local for kMinHops == kMaxHops == 2 without branches: both headers are read by every lane
+// (the second from a safe in-LDS address when the first is implausible or the chain leaves the staged
+// bytes) and the verdict is one select chain — the looped form's early returns made every
+// 64-candidate step pay exec-mask saves and restores for each hop.
+#ifndef PKTGPU_PCAP_BRANCHFREE
+#define PKTGPU_PCAP_BRANCHFREE 1
+#endif
+__device__ __forceinline__ int chain_local2(const uint32_t* lw, uint32_t c, uint32_t lend, uint32_t lim, uint32_t snap) {
+    if (c + 16 > lim) return 1;  // the file ends first (the caller guarantees c < lend)
+    const RecHdr h0 = hdr_lds(lw, c);
+    const bool ok0 = plausible32(h0, c, lim, snap);
+    const uint32_t p1 = c + 16 + h0.incl;  // < 2^22 past c when ok0 (incl <= 1 MiB)
+    const bool end1 = p1 + 16 > lim, far1 = p1 >= lend;
+    const RecHdr h1 = hdr_lds(lw, (ok0 & !end1 & !far1) ? p1 : c);
+    const bool ok1 = plausible32(h1, p1, lim, snap) & (h1.sec - h0.sec + kTsSpan <= 2 * kTsSpan);
+    return !ok0 ? 0 : end1 ? 1 : far1 ? 2 : (ok1 ? 1 : 0);
+}
+
 __device__ __forceinline__ bool chain_global(const uint32_t* lw, const uint8_t* buf, uint64_t lbase, uint64_t lend,
                                              uint64_t c, uint64_t stop, uint64_t len, uint32_t snap) {
     uint64_t p = c;
@@ -285,9 +303,13 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
         // The lowest candidate whose chain checks out inside the staged bytes wins; only when
         // there is none do the candidates whose chains leave them read global memory.
         const uint64_t c = c0 + lane;
-        const int r = c < stop && c + 16 <= len
-                          ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
-                          : 0;
+        int r = 0;
+        if constexpr (PKTGPU_PCAP_BRANCHFREE && kMinHops == 2 && kMaxHops == 2)
+            r = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
+        else
+            r = c < stop && c + 16 <= len
+                    ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
+                    : 0;
         uint64_t m = __ballot(r == 1);
         if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
         if (m) return c0 + (uint64_t)__builtin_ctzll(m);
@@ -319,23 +341,86 @@ __device__ __forceinline__ Agg region_agg(uint32_t k, uint32_t K, uint64_t entry
     return Agg{entry, exit, cw & 0x7FFFFFFFu, (cw >> 31) ? kBitErr : 0u};
 }
 
+// The walk of one region by ONE lane (pcap_guess_kernel): pkt_pcap_index's loop from `entry` while the
+// record starts inside [base, base + kRegion) and 16 header bytes remain, each record's offset from the
+// region base into lst[c].  32-bit positions relative to the staged bytes at lbase (the caller checks
+// that the file's end lies < 4 GiB past them).
+__device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, uint16_t* lst, uint64_t base,
+                                          uint64_t entry, uint64_t len, uint64_t& exit, uint32_t& cnt) {
+    const uint32_t rb = (uint32_t)(base - lbase), room = (uint32_t)(len - lbase) - rb;
+    const uint32_t lim = room >= 16 ? (room - 15 < kRegion ? room - 15 : kRegion) : 0u;
+    const uint32_t* lr = lw + (rb >> 2);
+    uint32_t q = entry >= base + kRegion ? kRegion : (uint32_t)(entry - base), c = 0, e = 0;
+    while (q < lim) {
+        const uint32_t k2 = (q >> 2) + 2;
+        const uint32_t incl = __builtin_amdgcn_alignbyte(lr[k2 + 1], lr[k2], q);
+        if (incl > room - 16 - q) {  // pkt_pcap_index: record runs past the end
+            e = 1;
+            q = room;
+            break;
+        }
+        lst[c] = (uint16_t)q;
+        c++;
+        q += 16 + incl;
+    }
+    exit = base + q;
+    cnt = c | (e ? 0x80000000u : 0u);
+}
+
 // GUESS (file header): one region per wave, a block stages 4 consecutive regions (16 KiB + 16 B).
 // (One wave per 8 KiB tile walking its second region on from the first's exit — half the candidate
 // scans — measured slower: 77 vs 63 us per 2^20-record call; the kernel is bound by each wave's
 // chain of dependent LDS reads, and the 32-waves-per-CU cap is reached either way.)
+// Round 4: after the four waves' candidate scans the block's four walks run on four LANES of wave 0
+// (one region each, in parallel) instead of each on a whole wave: a walk is a serial chain of ~20
+// dependent hops whose ~20 VALU instructions per hop a wave issued for all 64 lanes — two thirds of
+// the kernel's VALU work (628 per wave, profiles/pcap/r03ad_pcap_guess_pmc.txt).
+#ifndef PKTGPU_PCAP_LANEWALK
+#define PKTGPU_PCAP_LANEWALK 1
+#endif
 __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                          Scratch S) {
     constexpr uint32_t kStaged = kWaves * kRegion;
     __shared__ uint4 lds[kStaged / 16 + 2];
     __shared__ uint16_t lst[kWaves][kMaxRec];
+    __shared__ uint64_t s_entry[kWaves], s_exit[kWaves];
+    __shared__ uint32_t s_cnt[kWaves];
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     const uint64_t lbase = (uint64_t)blockIdx.x * kStaged;
     stage<kStaged, 256>(lds, buf, lbase, len, t);
     __syncthreads();
     const uint32_t k = blockIdx.x * kWaves + w;
-    if (k >= K) return;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     const uint64_t base = (uint64_t)k * kRegion;
+    if (PKTGPU_PCAP_LANEWALK && len - lbase <= 0xFFFFFFF0ull) {
+        const uint64_t entry = k >= K ? base + kRegion : (k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k));
+        if (lane == 0) s_entry[w] = entry;
+        __syncthreads();
+        if (w == 0 && lane < (uint32_t)kWaves) {
+            const uint32_t kk = blockIdx.x * kWaves + lane;
+            uint64_t ex = 0;
+            uint32_t cw = 0;
+            if (kk < K) lane_walk(lw, lbase, lst[lane], (uint64_t)kk * kRegion, s_entry[lane], len, ex, cw);
+            s_exit[lane] = ex;
+            s_cnt[lane] = cw;
+        }
+        __syncthreads();
+        if (k >= K) return;
+        const uint32_t cw = s_cnt[w], cnt = cw & 0x7FFFFFFFu;
+        uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+        for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
+        if (lane == 0) {
+            S.rentry[k] = entry;
+            S.rexit[k] = s_exit[w];
+            S.rcnt[k] = cw;
+            if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
+                const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
+                __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        return;
+    }
+    if (k >= K) return;
     const uint64_t entry = k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k);
     uint64_t exit;
     uint32_t cnt, err, rec;
