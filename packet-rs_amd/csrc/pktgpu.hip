@@ -237,6 +237,17 @@ __device__ __forceinline__ void emit_chain(const pkt_out_t& out, uint32_t i, uin
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+#ifndef PKTGPU_LATE_COLS
+#define PKTGPU_LATE_COLS 1  // parse_kernel loads its column bases after the walk (0: at the start)
+#endif
+#define KARG_AS __attribute__((address_space(4)))
+// A generic pointer the caller knows to be global memory, re-marked as such (addrspacecast to global
+// and back): loads and stores through it stay global_* instructions instead of flat_*.
+template <class T>
+__device__ __forceinline__ T* as_global(T* q) {
+    return (T*)((__attribute__((address_space(1))) T*)q);
+}
+
 // Diagnostic build only (-DPKTGPU_STAMPS=1: scripts/build_variant.sh, read by scripts/stamps.py): s_memtime stamps per wave of the
 // parse kernel — start, windows in LDS, walk done, emit issued, stores drained — plus the wave's
 // hardware id, written by lane 0 to a debug buffer no other code reads (pkt_debug_stamps).  In the
@@ -293,7 +304,7 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
-template <int NCH, uint32_t GM, int WK, bool STAGED = false>
+template <int NCH, uint32_t GM, int WK, bool STAGED = false, bool LATE = false>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own, uint64_t* pkt_st, const DispatchLds* T);
@@ -322,7 +333,7 @@ __host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9
 // (lockstep NCH = 7: 96-byte packed windows, 100 B per record, 26.2 KB per block: 6 blocks per CU;
 // NCH = 9: 128-byte windows, 33.8 KB: 4 blocks)
 // Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
-template <int NCH, uint32_t GM, int WK>
+template <int NCH, uint32_t GM, int WK, bool LATE = false>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
                                             uint64_t* pkt_st) {
     const uint32_t base = blk * (uint32_t)kBlock;  // within this launch
@@ -381,11 +392,11 @@ __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         PKT_STAMP(1);
-        parse_tile<NCH, GM, WK, true>(p, lds, base, chunk, off, len, act, pkt_st, T);
+        parse_tile<NCH, GM, WK, true, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T);
         return;
     }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM, WK>(p, lds, base, chunk, off, len, act, pkt_st, T);
+    parse_tile<NCH, GM, WK, false, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T);
 }
 
 template <int NCH, uint32_t GM, int WK>
@@ -395,7 +406,7 @@ void parse_kernel(KParams p) {
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
     PKT_STAMP(0);
     const DispatchLds* T = tables<WK>(lds, window_lds(NCH, WK), threadIdx.x, kBlock);
-    parse_block<NCH, GM, WK>(p, blockIdx.x, lds, T, pkt_st);
+    parse_block<NCH, GM, WK, PKTGPU_LATE_COLS != 0>(p, blockIdx.x, lds, T, pkt_st);
 }
 
 // ---- several batches in one launch (pkt_parse_batches) ----
@@ -439,7 +450,7 @@ void parse_multi_kernel(MultiParams mp) {
     parse_block<NCH, GM, WK>(p, blockIdx.x - b * mp.bpb, lds, T, pkt_st);
 }
 
-template <int NCH, uint32_t GM, int WK, bool STAGED>
+template <int NCH, uint32_t GM, int WK, bool STAGED, bool LATE>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
                                            bool active_own, uint64_t* pkt_st, const DispatchLds* T) {
@@ -524,12 +535,28 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         if ((t & 63u) == 0 && m) atomicMax(p.nh_max, m);
     }
     if (active_own) {
-        // (the column bases stay in SGPRs from the kernel start: C4 all columns keeps 106 SGPRs and
-        // spills 48 to VGPR lanes, ~96 lane instructions per wave; loading them after the walk
-        // through an opaque copy of the argument pointer made every column access a flat access:
-        // 6x slower, profiles/ab/r03j_late_column_pointers.txt)
-        emit_chain<GM>(out, i_own, len_own, r);
-        emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+        if constexpr (LATE) {
+            // The column bases are loaded here, after the walk, by scalar loads from the kernel
+            // arguments (an opaque copy of their address keeps the loads from being hoisted to the
+            // kernel start), and re-marked as global pointers so every store stays a global store.
+            // Loaded at the start instead, the 49 bases of the all-columns kernel held 106 SGPRs
+            // through the walk and spilled 48 to VGPR lanes (~96 lane instructions per wave); round
+            // 3's late load through a generic pointer made every column access a flat access, 6x
+            // slower (profiles/ab/r03j_late_column_pointers.txt).
+            // (parse_kernel's only argument is the KParams: it starts the kernarg segment)
+            uint64_t ka = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(KParams, out);
+            asm volatile("" : "+s"(ka));
+            const void* const KARG_AS* kc = reinterpret_cast<const void* const KARG_AS*>(ka);
+            pkt_out_t oc;
+            void** ocp = reinterpret_cast<void**>(&oc);
+#pragma unroll
+            for (int c = 0; c < 49; c++) ocp[c] = as_global(const_cast<void*>(kc[c]));
+            emit_chain<GM>(oc, i_own, len_own, r);
+            emit_fields<GM>(oc, i_own, pv_own, r, r.status == PKT_OK);
+        } else {
+            emit_chain<GM>(out, i_own, len_own, r);
+            emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
+        }
     }
 #if PKTGPU_STAMPS
     PKT_STAMP(3);
