@@ -202,6 +202,9 @@ __device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint6
 #ifndef PKTGPU_PACKED_WIN
 #define PKTGPU_PACKED_WIN 1  // 0: round 3's layout for every launch (A/B builds)
 #endif
+#ifndef PKTGPU_PACKED_MIN
+#define PKTGPU_PACKED_MIN 7  // narrowest packed lockstep build (chunks loaded; window 16 * (NCH - 1) bytes)
+#endif
 __host__ __device__ constexpr bool packed_win(int wk) { return PKTGPU_PACKED_WIN && wk == 1; }
 __host__ __device__ constexpr uint32_t lane_stride(int nch, int wk = 0) {
     return (uint32_t)(4 * (packed_win(wk) ? nch - 1 : nch) + 1) * 4u;
@@ -329,7 +332,9 @@ __device__ __forceinline__ const DispatchLds* tables(uint8_t* lds, size_t at, ui
 // windows (<= 64 VGPRs); for indexed windows what their LDS allows anyway — 6 for the 96-byte
 // windows (25.6 KB per block, 6 blocks per CU), 4 for the 144-byte ones (37.9 KB, 4 blocks); wider
 // windows unconstrained.
-__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : 6) : 8); }
+__host__ __device__ constexpr int waves_per_eu(int nch, int wk) {
+    return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : (PKTGPU_PACKED_WIN && nch == 6 ? 7 : 6)) : 8);
+}
 // (lockstep NCH = 7: 96-byte packed windows, 100 B per record, 26.2 KB per block: 6 blocks per CU;
 // NCH = 9: 128-byte windows, 33.8 KB: 4 blocks)
 // Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
@@ -532,7 +537,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     PKT_STAMP(2);
     if (p.nh_max) {  // wave-uniform: the used slot rows of the batch, for a gather of its chain
         const uint32_t m = wave_max_u32((active_own && r.status == PKT_OK) ? r.n : 0u);
-        if ((t & 63u) == 0 && m) atomicMax(p.nh_max, m);
+        if ((t & 63u) == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
     if (active_own) {
         if constexpr (LATE) {
@@ -658,7 +663,7 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     walk<WK>(pv, entry_state(p.entry), active, push, r, T);
     if (p.nh_max) {
         const uint32_t m = wave_max_u32((active && r.status == PKT_OK) ? r.n : 0u);
-        if (lane == 0 && m) atomicMax(p.nh_max, m);
+        if (lane == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
     if (!active) return;
     emit_chain<GM>(out, i, len, r);
@@ -698,7 +703,8 @@ hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream
     // lockstep (indexed batches; non-temporal column stores; packed windows): compiled for 7, 9 and
     // 17 loaded chunks only, i.e. 96-, 128- and 256-byte windows (parse_impl widens a narrower request)
     // (the A/B build without packed windows keeps round 3's set: 6, 9 and 17)
-    if constexpr (PKTGPU_PACKED_WIN ? (NCH >= 7) : (NCH >= 6 && NCH != 7)) if (wk == 1) {
+    if constexpr (PKTGPU_PACKED_WIN ? (NCH >= PKTGPU_PACKED_MIN && (NCH != 6 || PKTGPU_PACKED_MIN == 6))
+                                    : (NCH >= 6 && NCH != 7)) if (wk == 1) {
         switch (gm) {
             case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp);
             case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp);
@@ -793,14 +799,16 @@ __global__ __launch_bounds__(256) void max_hdrs_kernel(const uint8_t* nh, uint64
     }
 #pragma unroll
     for (int sft = 32; sft >= 1; sft >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, sft, 64));
-    if ((threadIdx.x & 63) == 0 && m) atomicMax(out, m);
+    if ((threadIdx.x & 63) == 0 && m) atomicMax(out + (blockIdx.x & (kMaxSpread - 1)), m);
 }
 
 hipError_t ensure_max_scratch(pkt_ctx* ctx) {
     if (ctx->mx.dev) return hipSuccess;
-    hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->mx.dev), MaxScratch::kWords * sizeof(uint32_t));
+    static_assert(MaxScratch::kSpread == (int)kMaxSpread, "one spread");
+    constexpr size_t bytes = MaxScratch::kGroups * MaxScratch::kSpread * sizeof(uint32_t);
+    hipError_t e = hipMalloc(reinterpret_cast<void**>(&ctx->mx.dev), bytes);
     if (e == hipSuccess)
-        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->mx.host), MaxScratch::kWords * sizeof(uint32_t),
+        e = hipHostMalloc(reinterpret_cast<void**>(&ctx->mx.host), bytes,
                           hipHostMallocDefault);
     if (e != hipSuccess) {
         (void)hipFree(ctx->mx.dev);
@@ -812,14 +820,15 @@ hipError_t ensure_max_scratch(pkt_ctx* ctx) {
 
 // Queue the reduction of n_hdrs[0, n) into scratch word `w` and its copy to the host mirror on `s`.
 hipError_t max_hdrs_async(pkt_ctx* ctx, const uint8_t* nh, uint64_t n, int w, hipStream_t s) {
-    hipError_t e = hipMemsetAsync(ctx->mx.dev + w, 0, sizeof(uint32_t), s);
+    hipError_t e = hipMemsetAsync(ctx->mx.dgroup(w), 0, MaxScratch::kSpread * sizeof(uint32_t), s);
     if (e != hipSuccess) return e;
     if (n) {
         const unsigned grid = (unsigned)std::min<uint64_t>((n + 4095) / 4096, 1024);
-        hipLaunchKernelGGL(max_hdrs_kernel, dim3(grid), dim3(256), 0, s, nh, n, ctx->mx.dev + w);
+        hipLaunchKernelGGL(max_hdrs_kernel, dim3(grid), dim3(256), 0, s, nh, n, ctx->mx.dgroup(w));
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
-    return hipMemcpyAsync(ctx->mx.host + w, ctx->mx.dev + w, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    return hipMemcpyAsync(ctx->mx.hgroup(w), ctx->mx.dgroup(w), MaxScratch::kSpread * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, s);
 }
 
 }  // namespace
@@ -840,11 +849,11 @@ int pkt_chain_max_hdrs(pkt_ctx_t* ctx, const uint8_t* n_hdrs, uint64_t n, uint32
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = ensure_max_scratch(ctx);
     if (e != hipSuccess) return hip_fail(ctx, e, "pkt_chain_max_hdrs scratch");
-    const int w = MaxScratch::kWords - 1;
+    const int w = MaxScratch::kGroups - 1;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if ((e = max_hdrs_async(ctx, n_hdrs, n, w, s)) != hipSuccess) return hip_fail(ctx, e, "max_hdrs_kernel");
     if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
-    *max_out = std::min<uint32_t>(ctx->mx.host[w], PKT_MAX_HDRS);
+    *max_out = std::min<uint32_t>(ctx->mx.host_max(w), PKT_MAX_HDRS);
     return PKT_SUCCESS;
 }
 
@@ -984,14 +993,16 @@ int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, con
     hipError_t e = hipSetDevice(ctx->device);
     if (e == hipSuccess) e = ensure_max_scratch(ctx);
     if (e != hipSuccess) return hip_fail(ctx, e, "parse rows scratch");
-    const int w = MaxScratch::kWords - 1;
+    const int w = MaxScratch::kGroups - 1;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if ((e = hipMemsetAsync(ctx->mx.dev + w, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
-    const int rc = parse_impl(ctx, b, entry, out, stream, 0, ctx->staging, ctx->mx.dev + w);
+    if ((e = hipMemsetAsync(ctx->mx.dgroup(w), 0, MaxScratch::kSpread * sizeof(uint32_t), s)) != hipSuccess)
+        return hip_fail(ctx, e, "hipMemsetAsync");
+    const int rc = parse_impl(ctx, b, entry, out, stream, 0, ctx->staging, ctx->mx.dgroup(w));
     if (rc != PKT_SUCCESS) return rc;
-    if ((e = hipMemcpyAsync(ctx->mx.host + w, ctx->mx.dev + w, sizeof(uint32_t), hipMemcpyDeviceToHost, s)) != hipSuccess)
+    if ((e = hipMemcpyAsync(ctx->mx.hgroup(w), ctx->mx.dgroup(w), MaxScratch::kSpread * sizeof(uint32_t),
+                            hipMemcpyDeviceToHost, s)) != hipSuccess)
         return hip_fail(ctx, e, "hipMemcpyAsync (rows)");
-    *rows_host = ctx->mx.host + w;
+    *rows_host = ctx->mx.hgroup(w);
     return PKT_SUCCESS;
 }
 
@@ -1022,7 +1033,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // the same 100 B of LDS per record as round 3's 80-byte window from the 16-byte-aligned start,
     // whose 96-byte form needed 148 B and 4 blocks per CU instead of 6; round-3 measurements of C4 per
     // 2^20 records, 2 streams: 80 B 68.1 us (all columns), 96 B 69.1 with 206 instead of 245 MB read).
-    if (w == 0) w = b->offsets ? (PKTGPU_PACKED_WIN ? 96u : 80u) : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
+    if (w == 0) w = b->offsets ? (PKTGPU_PACKED_WIN ? 16u * (PKTGPU_PACKED_MIN - 1) : 80u) : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);
@@ -1039,7 +1050,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
     // lockstep windows are packed from the packet's first byte: 16*(nch-1) packet bytes from nch
     // loaded chunks, at least 96 (the narrowest lockstep build, NCH = 7)
-    if (wk == 1) nch = PKTGPU_PACKED_WIN ? std::max<int>(7, (int)((w + 15) / 16) + 1) : std::max(nch, 6);
+    if (wk == 1) nch = PKTGPU_PACKED_WIN ? std::max<int>(PKTGPU_PACKED_MIN, (int)((w + 15) / 16) + 1) : std::max(nch, 6);
     for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kLaunchChunk) {
         const uint64_t cnt = std::min<uint64_t>(kLaunchChunk, b->n - i0);
         KParams kp;
@@ -1158,7 +1169,7 @@ static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const p
         if (slot_rows) {
             hipError_t es = hipEventSynchronize(hp.ev[q]);
             if (es != hipSuccess) return es;
-            rows = std::min<uint32_t>(ctx->mx.host[q], PKT_MAX_HDRS);
+            rows = std::min<uint32_t>(ctx->mx.host_max(q), PKT_MAX_HDRS);
         }
         for (int c : {kColHdrType, kColHdrOff}) {
             if (!hcol[c] || !rows) continue;
@@ -1213,11 +1224,11 @@ static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const p
         uint8_t** dcol = reinterpret_cast<uint8_t**>(&dout);
         for (int c = 0; c < 49; c++) dcol[c] = hcol[c] ? hp.out[q] + col_off[c] : nullptr;
         // (the device buffer always has >= 16 readable bytes, so a view shorter than 16 is safe)
-        if (slot_rows && (e = hipMemsetAsync(ctx->mx.dev + q, 0, sizeof(uint32_t), s)) != hipSuccess) {
+        if (slot_rows && (e = hipMemsetAsync(ctx->mx.dgroup(q), 0, MaxScratch::kSpread * sizeof(uint32_t), s)) != hipSuccess) {
             rc = hip_fail(ctx, e, "hipMemsetAsync");
             break;
         }
-        rc = parse_impl(ctx, &db, entry, &dout, s, bias, ctx->staging, slot_rows ? ctx->mx.dev + q : nullptr);
+        rc = parse_impl(ctx, &db, entry, &dout, s, bias, ctx->staging, slot_rows ? ctx->mx.dgroup(q) : nullptr);
         if (rc != PKT_SUCCESS) break;
         // out: every requested per-packet column into its host rows [lo, hi); the slot rows of this
         // chunk once its count is known (after the next chunk is queued)
@@ -1227,7 +1238,8 @@ static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const p
             e = hipMemcpyAsync(const_cast<uint8_t*>(hcol[c]) + lo * sz, dcol[c], m * sz, hipMemcpyDeviceToHost, s);
         }
         if (e == hipSuccess && slot_rows) {
-            e = hipMemcpyAsync(ctx->mx.host + q, ctx->mx.dev + q, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+            e = hipMemcpyAsync(ctx->mx.hgroup(q), ctx->mx.dgroup(q), MaxScratch::kSpread * sizeof(uint32_t),
+                               hipMemcpyDeviceToHost, s);
             if (e == hipSuccess) e = hipEventRecord(hp.ev[q], s);
         }
         if (e == hipSuccess && k > 0) e = copy_slots(k - 1);

@@ -52,12 +52,21 @@ inline uint64_t col_bytes(int c, uint64_t n) {
     return n * kColSize[c] * ((c == kColHdrType || c == kColHdrOff) ? PKT_MAX_HDRS : 1);
 }
 
-// Words of the slot-row reduction (pkt_chain_max_hdrs): one per host-pipeline slot + one for the
-// blocking call, on the device and mirrored in pinned host memory.
+// Words of the slot-row reductions (pkt_chain_max_hdrs, the fused maximum of the parse kernels): one
+// group of 256 words (kMaxSpread, pktgpu_device.hpp) per host-pipeline slot + one for the blocking
+// calls, on the device and mirrored in pinned host memory; a group's maximum is the max of its words.
 struct MaxScratch {
-    static constexpr int kWords = HostPipe::kSlots + 1;
+    static constexpr int kGroups = HostPipe::kSlots + 1;
+    static constexpr int kSpread = 256;
     uint32_t* dev = nullptr;
     uint32_t* host = nullptr;
+    uint32_t* dgroup(int g) const { return dev + g * kSpread; }
+    uint32_t* hgroup(int g) const { return host + g * kSpread; }
+    uint32_t host_max(int g) const {
+        uint32_t m = 0;
+        for (int k = 0; k < kSpread; k++) m = m > host[g * kSpread + k] ? m : host[g * kSpread + k];
+        return m;
+    }
 };
 
 struct pkt_ctx {
@@ -85,5 +94,6 @@ inline int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
 // pkt_parse_batch that also leaves the batch's largest n_hdrs (its used slot rows, <= PKT_MAX_HDRS
 // for a parsed packet) in pinned host memory: *rows_host is valid once `stream` has passed the call.
 // The reduction is fused into the parse kernel.  Used by the multi-GPU gather (pktgpu_mgpu.cpp).
+// *rows_host = the group of MaxScratch::kSpread pinned words whose maximum is the row count.
 int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
                             const uint32_t** rows_host);

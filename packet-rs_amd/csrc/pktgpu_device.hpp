@@ -57,8 +57,13 @@ struct KParams {
     int entry;
     int fast;  // register fast path for Ether/IPv4/UDP|TCP (entries PARSE / ETHERNET)
     pkt_out_t out;
-    uint32_t* nh_max;  // non-NULL: atomicMax of the batch's largest n_hdrs (the used slot rows) here
+    uint32_t* nh_max;  // non-NULL: the batch's largest n_hdrs (the used slot rows), spread over kMaxSpread
+                       // words (wave maxima atomicMax'ed into word blockIdx % kMaxSpread; the host
+                       // takes the max of the words)
 };
+// Words the n_hdrs maximum is spread over: one device-scope atomic per wave on ONE word serialised —
+// 2^18 of them took 2.6-3 ms per 2^24-packet parse (bench c5 r04a); spread over 256 words they do not.
+constexpr uint32_t kMaxSpread = 256;
 
 // The largest value of v over the wave (butterfly; every lane gets it).
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {

@@ -481,7 +481,9 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
             hipError_t e = hipSetDevice(mg->dev[i]);
             if (e == hipSuccess) e = hipStreamSynchronize(mg->stream[i]);
             if (e != hipSuccess) return mhip(mg, e, "hipStreamSynchronize (slot rows)");
-            rows[i] = std::min<uint32_t>(*rows_host[i], PKT_MAX_HDRS);
+            uint32_t m = 0;
+            for (int k = 0; k < MaxScratch::kSpread; k++) m = std::max(m, rows_host[i][k]);
+            rows[i] = std::min<uint32_t>(m, PKT_MAX_HDRS);
         }
         gather_plan(mask, nd, n.data(), rows.data(), merge, plan);
     }
