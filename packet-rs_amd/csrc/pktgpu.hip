@@ -192,38 +192,21 @@ __device__ __forceinline__ void packet_range(const KParams& p, uint32_t i, uint6
 // per-lane dword reads of the walk hit 64 distinct banks); +16 B for the last lane's over-read.
 // (A chunk-major layout with ds_write_b128 staging had 4-way conflicts on the walk's reads: C4
 // 3 % slower, C2/C3 neutral, scripts/ab_bench.sh.)
-// Lockstep (indexed-batch) launches PACK each window from the packet's first byte instead: NCH chunks
-// are loaded from the 16-byte-aligned start and packet bytes [0, 16*(NCH-1)) are stored at window
-// bytes [0, 16*(NCH-1)), whatever the start's alignment — the LDS holds 16 packet bytes per chunk of
-// the window instead of 16 - (off & 15) for the first one (C4: 96 packet bytes in 100 B per record
-// where the round-3 layout held 81-96 in the same space), and windows start 16 B into the region
-// (the guard below window 0 takes the first dword writes of an unaligned packet, the 4-byte pad after
-// each window the last ones).
-#ifndef PKTGPU_PACKED_WIN
-#define PKTGPU_PACKED_WIN 1  // 0: round 3's layout for every launch (A/B builds)
-#endif
-#ifndef PKTGPU_PACKED_MIN
-#define PKTGPU_PACKED_MIN 7  // narrowest packed lockstep build (chunks loaded; window 16 * (NCH - 1) bytes)
-#endif
-__host__ __device__ constexpr bool packed_win(int wk) { return PKTGPU_PACKED_WIN && wk == 1; }
-__host__ __device__ constexpr uint32_t lane_stride(int nch, int wk = 0) {
-    return (uint32_t)(4 * (packed_win(wk) ? nch - 1 : nch) + 1) * 4u;
-}
-__host__ __device__ constexpr uint32_t win_base(int wk) { return packed_win(wk) ? 16u : 0u; }
-__host__ __device__ constexpr size_t window_lds(int nch, int wk = 0) {
-    return ((size_t)win_base(wk) + (size_t)kBlock * lane_stride(nch, wk) + 16 + 15) & ~(size_t)15;
+__host__ __device__ constexpr uint32_t lane_stride(int nch) { return (uint32_t)(4 * nch + 1) * 4u; }
+__host__ __device__ constexpr size_t window_lds(int nch) {
+    return ((size_t)kBlock * lane_stride(nch) + 16 + 15) & ~(size_t)15;
 }
 
 __device__ __forceinline__ PacketView make_view(const KParams& p, uint8_t* lds, uint32_t q, uint64_t off,
-                                                uint32_t len, int nch, int wk = 0) {
+                                                uint32_t len, int nch) {
     PacketView pv;
-    pv.lw = lds + win_base(wk) + q * lane_stride(nch, wk);
+    pv.lw = lds + q * lane_stride(nch);
     pv.slab = p.slab;
     pv.off = off;
     pv.last4 = ((p.slab_len + 15) & ~(uint64_t)15) - 4;
-    pv.shift = packed_win(wk) ? 0u : (uint32_t)(off & 15);
+    pv.shift = (uint32_t)(off & 15);
     pv.win_lo = 0;
-    pv.win_end = packed_win(wk) ? (uint32_t)(nch - 1) * 16u : (uint32_t)nch * 16u - pv.shift;
+    pv.win_end = (uint32_t)nch * 16u - pv.shift;
     pv.len = len;
     return pv;
 }
@@ -332,11 +315,7 @@ __device__ __forceinline__ const DispatchLds* tables(uint8_t* lds, size_t at, ui
 // windows (<= 64 VGPRs); for indexed windows what their LDS allows anyway — 6 for the 96-byte
 // windows (25.6 KB per block, 6 blocks per CU), 4 for the 144-byte ones (37.9 KB, 4 blocks); wider
 // windows unconstrained.
-__host__ __device__ constexpr int waves_per_eu(int nch, int wk) {
-    return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : (PKTGPU_PACKED_WIN && nch == 6 ? 7 : 6)) : 8);
-}
-// (lockstep NCH = 7: 96-byte packed windows, 100 B per record, 26.2 KB per block: 6 blocks per CU;
-// NCH = 9: 128-byte windows, 33.8 KB: 4 blocks)
+__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : 6) : 8); }
 // Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
 template <int NCH, uint32_t GM, int WK, bool LATE = false>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
@@ -374,24 +353,11 @@ __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint
             uint64_t a = (offr & ~(uint64_t)15) + 16u * c;
             a = a > last16 ? last16 : a;
             const u32x4 v = *reinterpret_cast<const u32x4*>(p.slab + a);
-            if constexpr (packed_win(WK)) {
-                // packed window: aligned-stream byte 16c + x is packet byte 16c + x - shift; a dword
-                // is stored (unaligned LDS write) when it overlaps packet bytes [0, 16*(NCH-1))
-                uint8_t* w = lds + win_base(WK) + (wave0 + r) * lane_stride(NCH, WK);
-                const int32_t b0 = (int32_t)(16u * c) - (int32_t)(offr & 15);
-                const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    const int32_t b = b0 + 4 * j;
-                    if (b > -4 && b < 16 * (NCH - 1)) __builtin_memcpy(w + b, &d[j], 4);
-                }
-            } else {
-                uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH, WK)) + 4 * c;
-                w[0] = v.x;
-                w[1] = v.y;
-                w[2] = v.z;
-                w[3] = v.w;
-            }
+            uint32_t* w = reinterpret_cast<uint32_t*>(lds + (wave0 + r) * lane_stride(NCH)) + 4 * c;
+            w[0] = v.x;
+            w[1] = v.y;
+            w[2] = v.z;
+            w[3] = v.w;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -410,7 +376,7 @@ void parse_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
     PKT_STAMP(0);
-    const DispatchLds* T = tables<WK>(lds, window_lds(NCH, WK), threadIdx.x, kBlock);
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
     parse_block<NCH, GM, WK, PKTGPU_LATE_COLS != 0>(p, blockIdx.x, lds, T, pkt_st);
 }
 
@@ -440,7 +406,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_pe
 void parse_multi_kernel(MultiParams mp) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
-    const DispatchLds* T = tables<WK>(lds, window_lds(NCH, WK), threadIdx.x, kBlock);
+    const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
     const uint32_t b = blockIdx.x / mp.bpb;  // wave-uniform
     const MultiBatch& mb = mp.per[b];
     KParams p = mp.base;
@@ -471,13 +437,12 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
     bool fast = false, fudp = false;
     uint32_t fv = 0;
     if constexpr (NCH >= 4) {
-        // (packed windows hold packet dword k at window dword k whatever the alignment)
-        if (p.fast && active_own && (packed_win(WK) || (off_own & 15) == 0)) {
+        if (p.fast && active_own && (off_own & 15) == 0) {
             // dwords 3..11 of the packet (little-endian), from the registers or, when the wave
             // loaded its windows cooperatively, from the lane's own LDS window
             uint32_t d3, d4, d5, d6, d7, d9, d10, d11;
             if constexpr (STAGED) {
-                const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + win_base(WK) + t * lane_stride(NCH, WK));
+                const uint32_t* w = reinterpret_cast<const uint32_t*>(lds + t * lane_stride(NCH));
                 d3 = w[3], d4 = w[4], d5 = w[5], d6 = w[6], d7 = w[7], d9 = w[9], d10 = w[10], d11 = w[11];
             } else {
                 d3 = chunk[0].w, d4 = chunk[1].x, d5 = chunk[1].y, d6 = chunk[1].z, d7 = chunk[1].w;
@@ -525,7 +490,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         push(2 + v, fudp ? PKT_HDR_UDP : PKT_HDR_TCP, l4);
     };
     if constexpr (!STAGED) stage_window<NCH>(lds, t, chunk);
-    PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH, STAGED ? WK : 0);
+    PacketView pv_own = make_view(p, lds, t, off_own, len_own, NCH);
 
     // each lane walks and emits its own packet (no barrier: own LDS only)
     __builtin_amdgcn_wave_barrier();
@@ -682,14 +647,14 @@ template <int NCH, uint32_t GM, int WK>
 hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiParams* mp) {
     if (mp) {  // several batches, one launch (windows only)
         hipLaunchKernelGGL((parse_multi_kernel<NCH, GM, WK>), dim3(mp->bpb * mp->k), dim3(kBlock),
-                           with_tables(window_lds(NCH, WK), WK), s, *mp);
+                           with_tables(window_lds(NCH), WK), s, *mp);
         return hipGetLastError();
     }
     if (mode == M_SPAN) {
         hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), with_tables(span_region(NCH), WK), s, kp);
     } else {
-        const size_t lds = with_tables(window_lds(NCH, WK), WK);
+        const size_t lds = with_tables(window_lds(NCH), WK);
         hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }
@@ -700,11 +665,9 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiPa
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
 hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s, const MultiParams* mp) {
-    // lockstep (indexed batches; non-temporal column stores; packed windows): compiled for 7, 9 and
-    // 17 loaded chunks only, i.e. 96-, 128- and 256-byte windows (parse_impl widens a narrower request)
-    // (the A/B build without packed windows keeps round 3's set: 6, 9 and 17)
-    if constexpr (PKTGPU_PACKED_WIN ? (NCH >= PKTGPU_PACKED_MIN && (NCH != 6 || PKTGPU_PACKED_MIN == 6))
-                                    : (NCH >= 6 && NCH != 7)) if (wk == 1) {
+    // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 9 and
+    // 17 chunks only (parse_impl widens a narrower request)
+    if constexpr (NCH >= 6 && NCH != 7) if (wk == 1) {
         switch (gm) {
             case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp);
             case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp);
@@ -1029,11 +992,16 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // indexed: 128 B.  Unaligned packet starts need one more chunk.
     uint32_t w = ctx->window;
     // Auto window: the stride up to 64 bytes for fixed-stride slabs (Ether[/Vlan x2]/IPv4/TCP ends at
-    // byte 62); 96 packet bytes for indexed batches, packed from the record's first byte (round 4:
-    // the same 100 B of LDS per record as round 3's 80-byte window from the 16-byte-aligned start,
-    // whose 96-byte form needed 148 B and 4 blocks per CU instead of 6; round-3 measurements of C4 per
-    // 2^20 records, 2 streams: 80 B 68.1 us (all columns), 96 B 69.1 with 206 instead of 245 MB read).
-    if (w == 0) w = b->offsets ? (PKTGPU_PACKED_WIN ? 16u * (PKTGPU_PACKED_MIN - 1) : 80u) : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
+    // byte 62); 80 bytes for indexed batches (96 from the record's 16-byte-aligned start: every
+    // header of 16 of the 22 reference templates, the rest read past it through L2).  C4 per 2^20
+    // records, same box, 2 streams: 80 B 46.6 (chain) / 68.1 us (all columns), 64 B 49.4 / 75.8,
+    // 96 B 49.6 / 69.1, 128 B 59.7 / 77.4 — wider windows read fewer lines twice but hold fewer
+    // waves per CU (LDS), round 3.  (Round 4: windows packed from the record's first
+    // byte — 80 or 96 packet bytes in 84 or 100 B of LDS per record, 7 or 6 blocks per CU — were
+    // slower than this layout in every combination: C4 all columns 72.6-74.1 vs 69.9 us, chain
+    // 52.6-57.7 vs 50.4 us per 2-stream step; the unaligned LDS stores of the staging cost more than
+    // the occupancy or the lines they save, profiles/ab/r04c_c4_packed_windows.txt.)
+    if (w == 0) w = b->offsets ? 80u : std::min<uint32_t>(std::max<uint32_t>(b->stride, 16u), 64u);
     w = std::min<uint32_t>(std::max<uint32_t>((w + 15) & ~15u, 16u), 256u);
     bool aligned = !b->offsets && (b->stride % 16 == 0);
     int nch = (int)(w / 16) + (aligned ? 0 : 1);
@@ -1048,9 +1016,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
     // Walk: lockstep for indexed batches (pcap replays mix chains within a wave), waterfall for
     // fixed-stride slabs (one layout per wave), unless the ctx says otherwise.
     const int wk = ctx->walk == 2 ? 1 : ctx->walk == 1 ? 0 : (b->offsets ? 1 : 0);
-    // lockstep windows are packed from the packet's first byte: 16*(nch-1) packet bytes from nch
-    // loaded chunks, at least 96 (the narrowest lockstep build, NCH = 7)
-    if (wk == 1) nch = PKTGPU_PACKED_WIN ? std::max<int>(PKTGPU_PACKED_MIN, (int)((w + 15) / 16) + 1) : std::max(nch, 6);
+    if (wk == 1 && nch < 6) nch = 6;  // the narrowest lockstep build
     for (uint64_t i0 = 0; i0 < b->n && e == hipSuccess; i0 += kLaunchChunk) {
         const uint64_t cnt = std::min<uint64_t>(kLaunchChunk, b->n - i0);
         KParams kp;
@@ -1078,7 +1044,6 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         else if (nch <= 4) e = launch_gm<4>(kp, gm, md, wk, s, mp);
         else if (nch <= 5) e = launch_gm<5>(kp, gm, md, wk, s, mp);
         else if (nch <= 6) e = launch_gm<6>(kp, gm, md, wk, s, mp);
-        else if (nch <= 7 && (PKTGPU_PACKED_WIN || wk == 0)) e = launch_gm<7>(kp, gm, md, wk, s, mp);
         else if (nch <= 9) e = launch_gm<9>(kp, gm, md, wk, s, mp);
         else e = launch_gm<17>(kp, gm, md, wk, s, mp);
     }

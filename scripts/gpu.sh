@@ -72,7 +72,7 @@ for step in "$@"; do
     host)  run host 600 bash -c 'for c in c2 c4; do python scripts/hostpath_native.py --config $c --chunks 262144 || exit $?;
                python scripts/hostpath_native.py --config $c --pageable --chunks 131072,262144 || exit $?; done' ;;
     ab)    IFS=: read -r c v <<< "$arg"; run ab_${c:-c2} 900 bash scripts/ab.sh "${c:-c2}" "${v:-status;chain;all}" 2 ;;
-    abn)   IFS=: read -r c v names <<< "$arg"; run abn_${c} 900 bash scripts/ab_named.sh "$c" "${v:-all}" 3 ${names//,/ } ;;
+    abn)   IFS=: read -r c v names <<< "$arg"; run abn_${c}_$(echo "${v:-all}" | tr -c 'a-z0-9' '_') 900 bash scripts/ab_named.sh "$c" "${v:-all}" 3 ${names//,/ } ;;
     pcapn) IFS=: read -r names <<< "$arg"; run pcapn 600 bash -c 'for rep in 1 2 3; do for name in '"${names//,/ }"'; do
                lib=packet-rs_amd/lib/variants/$name.so; [ "$name" = main ] && lib=packet-rs_amd/lib/libpktgpu.so
                PKTGPU_LIB=$lib timeout -k 10 120 python scripts/pcap_index_bench.py --reps 20 | sed "s|^|$name |" || exit $?; done; done' ;;
