@@ -343,28 +343,22 @@ def host_record(P, torch, cols, n=1 << 20, reps=5):
 
 def pcap_record(P, torch, dev, n=1 << 20, reps=10):
     """The capture path of tests/pcap.rs:7-37 on the device as one step: a pcap file already in HBM
-    -> pkt_pcap_index_device (record boundaries) -> pkt_parse_batch of every record (all columns)."""
-    import ctypes
+    -> pkt_parse_pcap (pkt_pcap_index_device's kernels, then pkt_parse_batch of every record, all
+    columns, taking the record count from the device: one host synchronisation per step)."""
     from pktgpu import gen, schema
     buf, offs, lens = gen.gen_c4(n, seed=0x5EED0005)
     d_buf = torch.from_numpy(buf).to(dev)
     d_offs = torch.empty(n, dtype=torch.uint64, device=dev)
     d_lens = torch.empty(n, dtype=torch.uint32, device=dev)
-    cols = schema.COLUMN_NAMES
-    out = P.alloc(n, cols)
-    ostr = P.out_struct(out)
+    out = P.alloc(n, schema.COLUMN_NAMES)
     s = torch.cuda.current_stream(dev)
-    cnt = ctypes.c_uint64()
+    cnt = [0]
 
     def step():
-        P._check(P._L.pkt_pcap_index_device(P._ctx, d_buf.data_ptr(), d_buf.numel(), d_offs.data_ptr(),
-                                             d_lens.data_ptr(), n, ctypes.byref(cnt), P._stream(s)),
-                 "pkt_pcap_index_device")
-        P.launch(P._batch(d_buf, int(cnt.value), None, d_offs, d_lens), 0, ostr, s)
-        s.synchronize()
+        cnt[0], _, _, _ = P.parse_pcap(d_buf, n, out=out, offsets=d_offs, lens=d_lens, stream=s)
 
     step()
-    ok = int(cnt.value) == n and np.array_equal(d_offs.cpu().numpy(), offs)
+    ok = cnt[0] == n and np.array_equal(d_offs.cpu().numpy(), offs)
     ts = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -372,8 +366,8 @@ def pcap_record(P, torch, dev, n=1 << 20, reps=10):
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     return {"workload": f"C4 capture: {n} records of the 22 reference templates, {buf.size} B pcap file in HBM",
-            "step": "pkt_pcap_index_device (blocking: its record count comes back to the host) + "
-                    "pkt_parse_batch (all columns) + stream sync",
+            "step": "pkt_parse_pcap: pcap_guess_kernel + pcap_scan_kernel (record boundaries, written by the "
+                    "scan) + parse_kernel (all columns, record count read on the device); one blocking call",
             "ms_per_step": round(t * 1e3, 4), "Grecords/s": round(n / t / 1e9, 4),
             "file_GB/s": round(buf.size / t / 1e9, 2), "index_matches_host_indexer": bool(ok),
             "reps": reps, "timing": "wall clock per step, median"}

@@ -438,6 +438,16 @@ int pkt_pcap_index(const uint8_t *buf, uint64_t len, uint64_t *offsets, uint32_t
 int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint64_t *offsets,
                           uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
 
+/* The capture path of tests/pcap.rs:7-37 on a pcap file already in DEVICE memory, in one call:
+ * pkt_pcap_index_device into offsets / lens (device, [cap], cap >= 1), then fast::parse_<entry> of
+ * every record (an indexed batch over `buf` in place) into `out` (device columns sized for cap
+ * records, slot columns strided by cap).  The parse takes the record count from the device (its
+ * blocks past it exit), so the host waits once, for both; *n_out = the record count (> cap: only
+ * the first cap records are indexed and parsed).  Errors as pkt_pcap_index_device (nothing is
+ * parsed then).  Blocking. */
+int pkt_parse_pcap(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
+                   uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
+
 /* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
 uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
 

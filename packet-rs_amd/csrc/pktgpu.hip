@@ -321,7 +321,13 @@ template <int NCH, uint32_t GM, int WK, bool LATE = false>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
                                             uint64_t* pkt_st) {
     const uint32_t base = blk * (uint32_t)kBlock;  // within this launch
-    const bool act = base + threadIdx.x < p.n;
+    uint32_t n_eff = p.n;
+    if (p.n_dev) {  // wave-uniform: the count the device produced (scalar load)
+        const uint64_t nd = *p.n_dev;
+        n_eff = nd < (uint64_t)n_eff ? (uint32_t)nd : n_eff;
+        if (base >= n_eff) return;  // the whole block is past the count
+    }
+    const bool act = base + threadIdx.x < n_eff;
     u32x4 chunk[NCH];
     uint64_t off;
     uint32_t len;
@@ -574,7 +580,12 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     const uint32_t lane = threadIdx.x;
     const DispatchLds* T = tables<WK>(lds, span_region(NCH), lane, kSpanBlock);
     const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
-    const bool active = i < p.n;
+    uint32_t n_eff = p.n;
+    if (p.n_dev) {
+        const uint64_t nd = *p.n_dev;
+        n_eff = nd < (uint64_t)n_eff ? (uint32_t)nd : n_eff;
+    }
+    const bool active = i < n_eff;
     uint64_t off = 0;
     uint32_t len = 0;
     if (active) packet_range(p, i, off, len);
@@ -896,7 +907,7 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
 
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                       void* stream, uint64_t off_bias, int staging, uint32_t* nh_max = nullptr,
-                      uint64_t slot_stride = 0, MultiParams* mp = nullptr);
+                      uint64_t slot_stride = 0, MultiParams* mp = nullptr, const uint64_t* n_dev = nullptr);
 
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
@@ -946,6 +957,14 @@ int pkt_parse_batches(pkt_ctx_t* ctx, const pkt_batch_t* batches, uint32_t nbatc
 
 }  // extern "C"
 
+// (internal, pktgpu_ctx.hpp) pkt_parse_batch with the count from the device.
+int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
+                         const uint64_t* count_dev, uint64_t slot_stride) {
+    if (b && b->n && b->slab_len < 16) return fail(ctx, PKT_ERR_INVALID_ARG, "slab_len < 16");
+    if (count_dev && b && b->n > kLaunchChunk) return fail(ctx, PKT_ERR_INVALID_ARG, "device count over 2^26 packets");
+    return parse_impl(ctx, b, entry, out, stream, 0, ctx ? ctx->staging : 0, nullptr, slot_stride, nullptr, count_dev);
+}
+
 // (internal, pktgpu_ctx.hpp) pkt_parse_batch whose kernel also reduces the batch's largest n_hdrs
 // (a wave max + one atomicMax per wave, fused into the parse) into a ctx word, copied to the ctx's
 // pinned mirror on `stream`: *rows_host holds it once the stream has passed this call.
@@ -974,7 +993,7 @@ extern "C" {
 // `staging` = the ctx's knob, or the host path's override (wave spans over the link).
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                       void* stream, uint64_t off_bias, int staging, uint32_t* nh_max, uint64_t slot_stride,
-                      MultiParams* mp) {
+                      MultiParams* mp, const uint64_t* n_dev) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -1032,6 +1051,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         kp.entry = entry;
         kp.fast = ctx->fast && (entry == PKT_ENTRY_PARSE || entry == PKT_ENTRY_ETHERNET);
         kp.nh_max = nh_max;
+        kp.n_dev = n_dev;  // (one launch: n_dev is only passed for batches of n <= kLaunchChunk)
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         for (int c = 0; c < 49; c++)

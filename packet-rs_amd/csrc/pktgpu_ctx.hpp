@@ -97,3 +97,9 @@ inline int hip_fail(pkt_ctx* ctx, hipError_t e, const char* what) {
 // *rows_host = the group of MaxScratch::kSpread pinned words whose maximum is the row count.
 int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
                             const uint32_t** rows_host);
+
+// pkt_parse_batch with the record count taken on the device from *count_dev (blocks past it exit;
+// NULL = b->n) and the slot columns strided by slot_stride (0 = b->n).  One launch: b->n <= 2^26 when
+// count_dev is given.  Used by pkt_parse_pcap (pktgpu_pcap.hip).
+int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
+                         const uint64_t* count_dev, uint64_t slot_stride = 0);

@@ -57,6 +57,8 @@ struct KParams {
     int entry;
     int fast;  // register fast path for Ether/IPv4/UDP|TCP (entries PARSE / ETHERNET)
     pkt_out_t out;
+    const uint64_t* n_dev;  // non-NULL: the batch holds min(n, *n_dev) packets (a count produced on the
+                            // device, e.g. by the pcap indexer; blocks past it exit)
     uint32_t* nh_max;  // non-NULL: the batch's largest n_hdrs (the used slot rows), spread over kMaxSpread
                        // words (wave maxima atomicMax'ed into word blockIdx % kMaxSpread; the host
                        // takes the max of the words)

@@ -9,13 +9,14 @@
 // remain; a record running past the end is an error; a shorter tail is ignored.
 //
 // The record chain is sequential (each header says where the next one starts): speculation per
-// 4 KiB region, then an exact pass over the regions' states, then the output.  Three kernels, one
-// host read-back:
+// 4 KiB region, then an exact pass over the regions' states that also writes the records.  Two
+// kernels, one host read-back (or none: pkt_parse_pcap's parse takes the count on the device):
 //   GUESS (pcap_guess_kernel)  a block stages 4 consecutive regions (16 KiB) in LDS; each wave
 //            finds the first offset of its region from which a chain of plausible record headers
-//            runs (64 candidates per step, one per lane) — or "none" — and walks the records from
-//            it: per region entry, exit, count (+ error bit) and the records' u16 offsets.  Region
-//            0's entry is 24 by definition.  No block waits for another.
+//            runs (64 candidates per step, one per lane) — or "none" — and four lanes of wave 0 then
+//            walk the block's four regions from their entries: per region entry, exit, count (+ error
+//            bit) and the records' u16 offsets.  Region 0's entry is 24 by definition.  No block
+//            waits for another.
 //   SCAN (pcap_scan_kernel)  a block takes the next 256 regions (a ticket, so every lower block
 //            is already running) and composes their states (combine() below: associative, and it
 //            carries consistency — a region's state is exact iff its entry equals the exact exit of
@@ -26,10 +27,9 @@
 //            its exit (stage the 4 KiB, walk: a few us, rare).  The block publishes its aggregate,
 //            composes the published states of the blocks before it (256 per round trip, stopping at
 //            the nearest exact one), fixes its own first seam against that exact exit if needed,
-//            publishes its exact state, and writes each region's exact record prefix.  The last
-//            block writes the total and the error flag to pinned host words.
-//   EMIT (pcap_emit_kernel)  16 regions per block, one record per thread: offset = pos + 16,
-//            incl_len = next pos - pos - 16 (the last one from the region's exit).
+//            publishes its exact state, writes each region's exact record prefix and then its
+//            records (offset = pos + 16, incl_len = next pos - pos - 16).  The last block writes the
+//            total and the error flag to pinned host words and the parse's count to a device word.
 // tests/test_pcap_model.py restates the composition and the fixes and checks them against the host
 // indexer on captures built to defeat the guess.  HBM traffic ≈ the file once + 2 B/record of
 // record lists written and read + 12 B/record of output.
@@ -53,16 +53,24 @@ constexpr uint32_t kTsSpan = 86400;               // guess: consecutive ts_sec w
 enum : int { kHostMagic = 0, kHostTotal = 1, kHostErr = 2, kHostWords = 4 };
 
 // A scan block's published states: its aggregate (a_*) once its own seams are consistent, its
-// exact inclusive state (i_*) once it knows the exact exit before it.  meta = epoch << 8 | bits
-// (| 16 = published): states of older calls carry older epochs, so the array needs no per-call reset.
+// exact inclusive state (i_*) once it knows the exact exit before it.  EVERY field carries the call's
+// 16-bit epoch in its top 16 bits (values: 48 bits — file positions and counts below 2^48): each field
+// is written once per call, so a reader that sees the current epoch in every field of a state has that
+// state's final values whatever order the fields became visible in — no ordering between data and flag
+// is needed (round 3 published data, waited for the stores (s_waitcnt vmcnt(0)) and then a flag word,
+// which relied on gfx950 behaviour outside the HIP memory model).  States of older calls carry older
+// epochs, so the array needs no per-call reset (a full reset when the epoch wraps).
 struct alignas(64) BlkDesc {
-    uint64_t a_first, a_last, a_cnt, a_meta;
-    uint64_t i_last, i_cnt, i_meta, pad;
+    uint64_t a_first, a_last, a_cnt, a_bits;
+    uint64_t i_last, i_cnt, i_bits, pad;
 };
-enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4, kPublished = 16 };
+constexpr uint32_t kEpochBits = 16;
+constexpr uint64_t kValMask = (1ull << (64 - kEpochBits)) - 1;
+__host__ __device__ constexpr uint64_t tagged(uint32_t epoch, uint64_t v) { return ((uint64_t)epoch << (64 - kEpochBits)) | v; }
+__host__ __device__ constexpr uint32_t tag_of(uint64_t w) { return (uint32_t)(w >> (64 - kEpochBits)); }
+enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4 };
 
 constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
-constexpr uint32_t kEmitRegions = 16;   // regions per emit block
 
 struct Scratch {
     uint64_t* rentry;  // per region: the walk's entry (>= the region's end: no record starts in it)
@@ -73,6 +81,11 @@ struct Scratch {
     BlkDesc* blk;      // one per scan block
     uint32_t* ticket;  // the scan kernel's
     uint64_t* host;    // kHostWords pinned words (device address)
+    uint64_t* dev;     // device words: [0] the record count for a parse that follows on the device (0 after
+                       // an error), [1] the magic check (guess region 0)
+    uint64_t cap;      // records the output arrays hold
+    uint64_t* out_offsets;  // [cap] or NULL
+    uint32_t* out_lens;     // [cap] or NULL
     uint32_t epoch;
 };
 
@@ -318,9 +331,9 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
 }
 
 // Tile states cross XCDs (each XCD has its own L2): every access is a device-scope relaxed atomic
-// (performed at the device's coherence point), and a publication is ordered by waiting for the data
-// stores to complete before the flag store — no release/acquire fences, which on gfx950 write back /
-// invalidate the whole L2 at device scope.  (A single-pass form that did the look-back per 16 KiB
+// (performed at the device's coherence point); a state is valid when all its fields carry the call's
+// epoch (BlkDesc), so no release/acquire fences are needed — on gfx950 they write back / invalidate
+// the whole L2 at device scope (1.18 ms per call when round 3 tried them).  (A single-pass form that did the look-back per 16 KiB
 // tile with a ticket per tile measured 160-436 us per 2^20-record call: 11.9K device-scope atomics
 // on one word serialise, and exact states can only advance 64 tiles per round trip.)
 template <class T>
@@ -331,7 +344,6 @@ template <class T>
 __device__ __forceinline__ void st_agent(T* p, T v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void vm_drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Region k's aggregate from its (entry, exit, count|err) state; identity past the file.
 __device__ __forceinline__ Agg region_agg(uint32_t k, uint32_t K, uint64_t entry, uint64_t exit, uint32_t cw) {
@@ -416,6 +428,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
                 const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
                 __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                S.dev[1] = mg;
             }
         }
         return;
@@ -442,6 +455,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
             const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
             __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            S.dev[1] = mg;
         }
     }
 }
@@ -584,11 +598,10 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     // ---- publish the aggregate; compose the blocks before (stopping at the nearest exact one)
     BlkDesc* my = S.blk + blk;
     if (t == 0) {
-        st_agent(&my->a_first, total.first);
-        st_agent(&my->a_last, total.last);
-        st_agent(&my->a_cnt, total.cnt);
-        vm_drain();
-        st_agent(&my->a_meta, ((uint64_t)S.epoch << 8) | kPublished | total.bits);
+        st_agent(&my->a_first, tagged(S.epoch, total.first));
+        st_agent(&my->a_last, tagged(S.epoch, total.last));
+        st_agent(&my->a_cnt, tagged(S.epoch, total.cnt));
+        st_agent(&my->a_bits, tagged(S.epoch, total.bits));
     }
     Agg P = agg_identity();
     for (;;) {
@@ -604,17 +617,20 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             Agg a = agg_identity();
             uint64_t xl = 0, xc = 0, xm = 0;
             if (jj >= 0) {
+                // all seven fields in one round trip; a state counts only with the epoch in every field
                 const BlkDesc* d = S.blk + jj;
-                const uint64_t im = ld_agent(&d->i_meta), am = ld_agent(&d->a_meta);
-                vm_drain();
-                if ((uint32_t)(im >> 8) == S.epoch) {
+                const uint64_t il_ = ld_agent(&d->i_last), ic_ = ld_agent(&d->i_cnt), ib_ = ld_agent(&d->i_bits);
+                const uint64_t af = ld_agent(&d->a_first), al = ld_agent(&d->a_last), ac = ld_agent(&d->a_cnt),
+                               ab = ld_agent(&d->a_bits);
+                const uint32_t ep = S.epoch;
+                if (tag_of(il_) == ep && tag_of(ic_) == ep && tag_of(ib_) == ep) {
                     st = 2;
-                    xl = ld_agent(&d->i_last);
-                    xc = ld_agent(&d->i_cnt);
-                    xm = im;
-                } else if ((uint32_t)(am >> 8) == S.epoch) {
+                    xl = il_ & kValMask;
+                    xc = ic_ & kValMask;
+                    xm = ib_ & kValMask;
+                } else if (tag_of(af) == ep && tag_of(al) == ep && tag_of(ac) == ep && tag_of(ab) == ep) {
                     st = 1;
-                    a = Agg{ld_agent(&d->a_first), ld_agent(&d->a_last), ld_agent(&d->a_cnt), (uint32_t)am & 15u};
+                    a = Agg{af & kValMask, al & kValMask, ac & kValMask, (uint32_t)(ab & 15u)};
                 }
             }
             // the nearest exact block in the window (the smallest thread index with st == 2)
@@ -708,19 +724,27 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     const uint32_t err_all = (P.bits | all.bits) & kBitErr;
     const uint64_t last = (all.bits & kBitNone) ? P.last : all.last;
     if (t == 0) {
-        st_agent(&my->i_last, last);
-        st_agent(&my->i_cnt, c_before + total.cnt);
-        vm_drain();
-        st_agent(&my->i_meta, ((uint64_t)S.epoch << 8) | kPublished | err_all);
+        st_agent(&my->i_last, tagged(S.epoch, last));
+        st_agent(&my->i_cnt, tagged(S.epoch, c_before + total.cnt));
+        st_agent(&my->i_bits, tagged(S.epoch, err_all));
         if (blk == nb - 1) {
             // every block has taken its ticket by now (this one took the last): the next call's
             // tickets start at 0 without a memset launch on the call's critical path (4.7 us)
             if (ticket) st_agent(S.ticket, 0u);
             __hip_atomic_store(&S.host[kHostTotal], c_before + total.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            // the count a parse on the same stream reads (kernel boundary: no fence needed); 0 when
+            // the call fails (bad magic, a record past the end), so that parse writes nothing
+            S.dev[0] = (S.dev[1] && !err_all) ? c_before + total.cnt : 0;
             __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err_all ? 1 : 0), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
+    // each region's exact record prefix, and the block's records themselves (offset = pos + 16,
+    // incl_len = next pos - pos - 16, the last one of a region from its exit): 256 threads write the
+    // block's records in order, one per thread per step (coalesced), the region found by a binary
+    // search over the block-relative prefixes (round 3 did this in a third kernel, 7.3 us per 2^20
+    // records)
+    __shared__ uint32_t epre[kScanRegions];
     {
         uint32_t x = k < K ? (scw[t] & 0x7FFFFFFFu) : 0u, c = x;
 #pragma unroll
@@ -730,66 +754,49 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         if (lane == 63) csum[w] = x;
         __syncthreads();
-        uint64_t before = c_before;
-        for (uint32_t q = 0; q < w; q++) before += csum[q];
-        if (k < K) S.rpre[k] = before + x - c;
-    }
-}
-
-// Emit (file header: EMIT): 256 threads write the records of 16 consecutive regions, one record per
-// thread per step, contiguous in the output (coalesced), at the regions' exact prefix.
-__global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
-                                                        uint64_t* __restrict__ offsets,
-                                                        uint32_t* __restrict__ lens) {
-    __shared__ uint32_t cpre[kEmitRegions + 1];
-    const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
-    if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
-        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & 0x7FFFFFFFu) : 0;
-        uint32_t x = c;
-#pragma unroll
-        for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (t >= d) x += y;
+        uint32_t bw = 0, btot = 0;
+        for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {
+            bw += q < w ? csum[q] : 0u;
+            btot += csum[q];
         }
-        if (t < kEmitRegions) cpre[t] = x - c;
-        if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
-    }
-    __syncthreads();
-    const uint64_t first = S.rpre[k0];
-    const uint32_t total = cpre[kEmitRegions];
-    for (uint32_t i = t; i < total; i += 256) {
-        const uint64_t idx = first + i;
-        if (idx >= cap) break;
-        uint32_t r = 0;
+        epre[t] = bw + x - c;
+        if (k < K) S.rpre[k] = c_before + bw + x - c;
+        __syncthreads();
+        if (S.out_offsets) {
+            for (uint32_t rr = t; rr < btot; rr += kScanRegions) {
+                const uint64_t idx = c_before + rr;
+                if (idx >= S.cap) break;
+                uint32_t j = 0;
 #pragma unroll
-        for (uint32_t b = kEmitRegions / 2; b; b >>= 1)
-            if (cpre[r + b] <= i) r += b;
-        const uint32_t k = k0 + r, li = i - cpre[r], c = cpre[r + 1] - cpre[r];
-        const uint64_t base = (uint64_t)k * kRegion;
-        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
-        const uint64_t pos = base + list[li];
-        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.rexit[k];
-        offsets[idx] = pos + 16;
-        lens[idx] = (uint32_t)(next - pos - 16);
+                for (uint32_t b = kScanRegions / 2; b; b >>= 1)
+                    if (j + b < kScanRegions && epre[j + b] <= rr) j += b;
+                const uint32_t kk = blk * kScanRegions + j, li = rr - epre[j], cj = scw[j] & 0x7FFFFFFFu;
+                const uint64_t base = (uint64_t)kk * kRegion;
+                const uint16_t* list = S.list + (uint64_t)kk * kMaxRec;
+                const uint64_t pos = base + list[li];
+                const uint64_t next = li + 1 < cj ? base + list[li + 1] : sex[j];
+                S.out_offsets[idx] = pos + 16;
+                S.out_lens[idx] = (uint32_t)(next - pos - 16);
+            }
+        }
     }
 }
 
 }  // namespace
 
-extern "C" {
-
-int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                          uint64_t cap, uint64_t* n_out, void* stream) {
-    if (!ctx || !buf || !n_out || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
-    *n_out = 0;
+// Queue the index of the pcap file `buf` on `s` (guess + scan kernels; the scan writes the records):
+// no host synchronisation.  *count_dev = the device word a following parse may take its record count
+// from (0 after an error).  pcap_finish reads the outcome once the stream is synchronised.
+static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev) {
+    if (!ctx || !buf || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
     const uint64_t K64 = (len + kRegion - 1) / kRegion;
-    if (K64 > (1ull << 31)) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
+    if (K64 > (1ull << 31) || len >= kValMask) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
     const uint32_t K = (uint32_t)K64, nb = (K + kScanRegions - 1) / kScanRegions;
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
     // Scratch: the ticket, the scan blocks' states, per-region states, prefixes and record lists.
     // The layout is fixed by the ALLOCATED capacity (k_cap regions, nb_cap block states), not by
@@ -820,7 +827,7 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     }
     // a new epoch per call (block states of older calls are ignored, not cleared; the block-state
     // area only ever holds epoch-tagged states, reset in full on wrap)
-    if (++pc.epoch >= (1u << 24)) {
+    if (++pc.epoch >= (1u << kEpochBits)) {
         pc.epoch = 1;
         if ((e = hipMemsetAsync(pc.buf, 0, pc.bytes, s)) != hipSuccess) return hip_fail(ctx, e, "hipMemset (pcap index)");
     }
@@ -839,6 +846,10 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     p += 4ull * pc.k_cap;
     S.list = reinterpret_cast<uint16_t*>(p);
     S.host = pc.ctl_dev;
+    S.dev = reinterpret_cast<uint64_t*>(static_cast<char*>(pc.buf) + 16);
+    S.cap = cap;
+    S.out_offsets = cap ? offsets : nullptr;
+    S.out_lens = cap ? lens : nullptr;
     S.epoch = pc.epoch;
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
@@ -852,14 +863,70 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     }
     // (tickets serialise: 186 device-scope atomics on one word cost the last block ~2.4 us)
     hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
-    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
-    if ((e = hipStreamSynchronize(s)) != hipSuccess) return hip_fail(ctx, e, "pcap index");
+    if (count_dev) *count_dev = S.dev;
+    return PKT_SUCCESS;
+}
+
+// The outcome of the last pcap_launch (the stream has been synchronised).
+static int pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) {
+    const PcapScratch& pc = ctx->pc;
     if (!pc.ctl[kHostMagic]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
     if (pc.ctl[kHostErr]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
     *n_out = pc.ctl[kHostTotal];
     return PKT_SUCCESS;
+}
+
+extern "C" {
+
+int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                          uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    *n_out = 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc = pcap_launch(ctx, buf, len, offsets, lens, cap, s, nullptr);
+    if (rc != PKT_SUCCESS) return rc;
+    const hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
+    return pcap_finish(ctx, n_out);
+}
+
+int pkt_parse_pcap(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                   uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!ctx || !out || !n_out || !cap || !offsets || !lens) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    *n_out = 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t* count_dev = nullptr;
+    int rc = pcap_launch(ctx, buf, len, offsets, lens, cap, s, &count_dev);
+    if (rc != PKT_SUCCESS) return rc;
+    pkt_batch_t b;
+    b.slab = buf;
+    b.slab_len = len;
+    b.offsets = offsets;
+    b.lens = lens;
+    b.stride = 0;
+    b.reserved = 0;
+    b.n = cap;
+    if (cap <= (1ull << 26)) {
+        // one parse launch over cap records whose blocks past the device-produced count exit: the
+        // host waits once, for the index and the parse together
+        rc = pktgpu_parse_counted(ctx, &b, entry, out, stream, count_dev);
+        if (rc != PKT_SUCCESS) return rc;
+        const hipError_t e = hipStreamSynchronize(s);
+        if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap");
+        return pcap_finish(ctx, n_out);
+    }
+    // batches over 2^26 records take several launches: the count first
+    hipError_t e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap");
+    if ((rc = pcap_finish(ctx, n_out)) != PKT_SUCCESS) return rc;
+    b.n = std::min(*n_out, cap);
+    rc = pktgpu_parse_counted(ctx, &b, entry, out, stream, nullptr, cap);
+    if (rc != PKT_SUCCESS) return rc;
+    e = hipStreamSynchronize(s);
+    return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "pkt_parse_pcap");
 }
 
 }  // extern "C"

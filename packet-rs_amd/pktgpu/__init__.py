@@ -204,6 +204,27 @@ class Parser:
                     "pkt_parse_host")
         return out
 
+    def parse_pcap(self, buf, cap=None, entry="parse", columns="all", out=None, offsets=None, lens=None,
+                   stream=None):
+        """pkt_parse_pcap: a pcap file in the uint8 device tensor `buf` -> (n records, {column: device
+        tensor} sized for cap records (slot columns [16][cap]), offsets, lens), index and parse in one
+        call with one host synchronisation.  cap=None: the file's size bounds the count (>= 16 B per
+        record), which sizes the outputs."""
+        torch = _torch()
+        assert buf.dtype == torch.uint8 and buf.is_cuda and buf.is_contiguous()
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        if cap is None:
+            cap = max(1, (buf.numel() - 24) // 16)
+        res = out if out is not None else self.alloc(cap, columns)
+        o = self.out_struct(res)
+        offsets = offsets if offsets is not None else torch.empty(cap, dtype=torch.uint64, device=self.torch_device)
+        lens = lens if lens is not None else torch.empty(cap, dtype=torch.uint32, device=self.torch_device)
+        n = ctypes.c_uint64()
+        self._check(self._L.pkt_parse_pcap(self._ctx, buf.data_ptr(), buf.numel(), e, ctypes.byref(o),
+                                           offsets.data_ptr(), lens.data_ptr(), int(cap), ctypes.byref(n),
+                                           self._stream(stream)), "pkt_parse_pcap")
+        return n.value, res, offsets, lens
+
     def parse_pcap_host(self, buf, cap, entry="parse", columns="all", out=None, index=True):
         """pkt_parse_pcap_host: a pcap file in host memory (numpy uint8 / bytes; pinned via host_empty
         for the full link rate) -> (n records, {column: numpy array} sized for `cap` records, slot

@@ -166,3 +166,40 @@ def test_one_ctx_growing_and_shrinking_captures():
             assert np.array_equal(l.cpu().numpy(), lens), (rep, n)
     finally:
         P2.close()
+
+
+def test_parse_pcap_fused_vs_oracle(P):
+    """pkt_parse_pcap: device index + parse in one call, the parse taking the record count from the
+    device (one host synchronisation).  Columns sized for cap > count: slot rows strided by cap and
+    nothing written past the count; cap < count; the errors parse nothing."""
+    import torch
+    n = 50000
+    buf, offs, lens = gen.gen_c4(n, seed=71)
+    cap = n + 777
+    res = P.alloc(cap, "all")
+    for v in res.values():
+        v.view(torch.uint8).fill_(0xEE)
+    m, g, o, l = P.parse_pcap(dev(buf), cap, out=res)
+    assert m == n
+    assert np.array_equal(o[:n].cpu().numpy(), offs) and np.array_equal(l[:n].cpu().numpy(), lens)
+    ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    for k, ov in ref.items():
+        gv = g[k].cpu().numpy()
+        if k in ("hdr_type", "hdr_off"):
+            valid = np.arange(schema.MAX_HDRS)[:, None] < ref["n_hdrs"].astype(np.int64)[None, :]
+            assert not (valid & (gv[:, :n] != ov)).any(), k
+        else:
+            assert np.array_equal(gv[:n], ov), k
+            assert (gv[n:].view(np.uint8) == 0xEE).all(), k  # past the count: untouched
+    m, g, o, l = P.parse_pcap(dev(buf), 1000, columns=["chain"])
+    assert m == n and np.array_equal(o.cpu().numpy(), offs[:1000])
+    ref = oracle.parse_batch(buf, 1000, offsets=offs[:1000], lens=lens[:1000], columns=list(g), nthreads=8)
+    for k in ("status", "n_hdrs", "payload_off", "payload_len"):
+        assert np.array_equal(g[k].cpu().numpy(), ref[k]), k
+    good = records([b"\x01" * 60, b"\x02" * 70, b"\x03" * 80])
+    for bad in (good[:-3], b"\x00" * 40):
+        res = P.alloc(8, ["status"])
+        res["status"].fill_(0xEE)
+        with pytest.raises(RuntimeError):
+            P.parse_pcap(dev(bad), 8, out=res)
+        assert (res["status"].cpu().numpy() == 0xEE).all()  # an error parses nothing
