@@ -9,8 +9,8 @@
 // remain; a record running past the end is an error; a shorter tail is ignored.
 //
 // The record chain is sequential (each header says where the next one starts): speculation per
-// 4 KiB region, then an exact pass over the regions' states that also writes the records.  Two
-// kernels, one host read-back (or none: pkt_parse_pcap's parse takes the count on the device):
+// 4 KiB region, then an exact pass over the regions' states, then the output.  Three kernels, one
+// host read-back (or none: pkt_parse_pcap's parse takes the count on the device):
 //   GUESS (pcap_guess_kernel)  a block stages 4 consecutive regions (16 KiB) in LDS; each wave
 //            finds the first offset of its region from which a chain of plausible record headers
 //            runs (64 candidates per step, one per lane) — or "none" — and four lanes of wave 0 then
@@ -27,9 +27,11 @@
 //            its exit (stage the 4 KiB, walk: a few us, rare).  The block publishes its aggregate,
 //            composes the published states of the blocks before it (256 per round trip, stopping at
 //            the nearest exact one), fixes its own first seam against that exact exit if needed,
-//            publishes its exact state, writes each region's exact record prefix and then its
-//            records (offset = pos + 16, incl_len = next pos - pos - 16).  The last block writes the
-//            total and the error flag to pinned host words and the parse's count to a device word.
+//            publishes its exact state and writes each region's exact record prefix.  The last
+//            block writes the total and the error flag to pinned host words and the parse's count
+//            to a device word.
+//   EMIT (pcap_emit_kernel)  16 regions per block, one record per thread: offset = pos + 16,
+//            incl_len = next pos - pos - 16 (the last one from the region's exit).
 // tests/test_pcap_model.py restates the composition and the fixes and checks them against the host
 // indexer on captures built to defeat the guess.  HBM traffic ≈ the file once + 2 B/record of
 // record lists written and read + 12 B/record of output.
@@ -71,6 +73,7 @@ __host__ __device__ constexpr uint32_t tag_of(uint64_t w) { return (uint32_t)(w 
 enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4 };
 
 constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
+constexpr uint32_t kEmitRegions = 16;   // regions per emit block
 
 struct Scratch {
     uint64_t* rentry;  // per region: the walk's entry (>= the region's end: no record starts in it)
@@ -83,9 +86,6 @@ struct Scratch {
     uint64_t* host;    // kHostWords pinned words (device address)
     uint64_t* dev;     // device words: [0] the record count for a parse that follows on the device (0 after
                        // an error), [1] the magic check (guess region 0)
-    uint64_t cap;      // records the output arrays hold
-    uint64_t* out_offsets;  // [cap] or NULL
-    uint32_t* out_lens;     // [cap] or NULL
     uint32_t epoch;
 };
 
@@ -739,12 +739,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    // each region's exact record prefix, and the block's records themselves (offset = pos + 16,
-    // incl_len = next pos - pos - 16, the last one of a region from its exit): 256 threads write the
-    // block's records in order, one per thread per step (coalesced), the region found by a binary
-    // search over the block-relative prefixes (round 3 did this in a third kernel, 7.3 us per 2^20
-    // records)
-    __shared__ uint32_t epre[kScanRegions];
+    // each region's exact record prefix (the emit kernel writes the records)
     {
         uint32_t x = k < K ? (scw[t] & 0x7FFFFFFFu) : 0u, c = x;
 #pragma unroll
@@ -754,33 +749,50 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         if (lane == 63) csum[w] = x;
         __syncthreads();
-        uint32_t bw = 0, btot = 0;
-        for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {
-            bw += q < w ? csum[q] : 0u;
-            btot += csum[q];
-        }
-        epre[t] = bw + x - c;
-        if (k < K) S.rpre[k] = c_before + bw + x - c;
-        __syncthreads();
-        if (S.out_offsets) {
-            for (uint32_t rr = t; rr < btot; rr += kScanRegions) {
-                const uint64_t idx = c_before + rr;
-                if (idx >= S.cap) break;
-                uint32_t j = 0;
-#pragma unroll
-                for (uint32_t b = kScanRegions / 2; b; b >>= 1)
-                    if (j + b < kScanRegions && epre[j + b] <= rr) j += b;
-                const uint32_t kk = blk * kScanRegions + j, li = rr - epre[j], cj = scw[j] & 0x7FFFFFFFu;
-                const uint64_t base = (uint64_t)kk * kRegion;
-                const uint16_t* list = S.list + (uint64_t)kk * kMaxRec;
-                const uint64_t pos = base + list[li];
-                const uint64_t next = li + 1 < cj ? base + list[li + 1] : sex[j];
-                S.out_offsets[idx] = pos + 16;
-                S.out_lens[idx] = (uint32_t)(next - pos - 16);
-            }
-        }
+        uint64_t before = c_before;
+        for (uint32_t q = 0; q < w; q++) before += csum[q];
+        if (k < K) S.rpre[k] = before + x - c;
     }
 }
+
+// Emit (file header: EMIT): 256 threads write the records of 16 consecutive regions, one record per
+// thread per step, contiguous in the output (coalesced), at the regions' exact prefix.
+__global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
+                                                        uint64_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ lens) {
+    __shared__ uint32_t cpre[kEmitRegions + 1];
+    const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
+    if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
+        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & 0x7FFFFFFFu) : 0;
+        uint32_t x = c;
+#pragma unroll
+        for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (t >= d) x += y;
+        }
+        if (t < kEmitRegions) cpre[t] = x - c;
+        if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
+    }
+    __syncthreads();
+    const uint64_t first = S.rpre[k0];
+    const uint32_t total = cpre[kEmitRegions];
+    for (uint32_t i = t; i < total; i += 256) {
+        const uint64_t idx = first + i;
+        if (idx >= cap) break;
+        uint32_t r = 0;
+#pragma unroll
+        for (uint32_t b = kEmitRegions / 2; b; b >>= 1)
+            if (cpre[r + b] <= i) r += b;
+        const uint32_t k = k0 + r, li = i - cpre[r], c = cpre[r + 1] - cpre[r];
+        const uint64_t base = (uint64_t)k * kRegion;
+        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
+        const uint64_t pos = base + list[li];
+        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.rexit[k];
+        offsets[idx] = pos + 16;
+        lens[idx] = (uint32_t)(next - pos - 16);
+    }
+}
+
 
 }  // namespace
 
@@ -847,9 +859,6 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     S.list = reinterpret_cast<uint16_t*>(p);
     S.host = pc.ctl_dev;
     S.dev = reinterpret_cast<uint64_t*>(static_cast<char*>(pc.buf) + 16);
-    S.cap = cap;
-    S.out_offsets = cap ? offsets : nullptr;
-    S.out_lens = cap ? lens : nullptr;
     S.epoch = pc.epoch;
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
@@ -863,6 +872,10 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     }
     // (tickets serialise: 186 device-scope atomics on one word cost the last block ~2.4 us)
     hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
+    // (the records written by the scan blocks themselves, after their look-back, measured slower:
+    // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
+    // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
+    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
     if (count_dev) *count_dev = S.dev;
