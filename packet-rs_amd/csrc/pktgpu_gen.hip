@@ -61,6 +61,24 @@ struct GenField {
     const uint64_t* values;  // PKT_GEN_VALUES: [n] of this launch
 };
 
+// A field's placement in the region kernel's LDS row, precomputed on the host by pkt_gen_create (the
+// field's position is the same for every packet): for each of the <= 2 pieces its bits overlap, the
+// piece's byte offset in the row, where the value's bit 0 lands in the piece's 128-bit big-endian
+// integer (sh, from its LSB; negative = right shift) and the field's bits there (m).  The kernel then
+// sets a field with one uniform shift of the value, an and-not and an or — round 3 rebuilt the masks
+// and shifts per field in every wave (932 SALU + 890 VALU instructions per wave for 11 fields and a
+// checksum, r04h PMC).
+struct GenPut {
+    uint32_t lds_off;
+    int32_t sh;
+    uint64_t mhi, mlo;
+};
+struct GenFieldPlan {
+    GenPut p[2];
+    uint32_t np;
+    uint32_t pad[3];
+};
+
 struct GenParams {
     const uint8_t* tpl;   // device template, zero-padded to tpl_bytes (a multiple of 16)
     uint8_t* dst;         // first packet of this launch
@@ -74,6 +92,8 @@ struct GenParams {
     uint32_t npkts;       // packets of this launch (gen_region_kernel)
     uint32_t nf, ncs;
     uint32_t csum_at[kMaxGenCsum];  // byte offset of each refreshed IPv4 header
+    uint32_t csum_lds[kMaxGenCsum];  // gen_region_kernel: that header's byte offset in the LDS row
+    const GenFieldPlan* plan;  // gen_region_kernel: [nf] (device)
     GenField f[kMaxGenFields];
 };
 
@@ -199,30 +219,38 @@ __global__ __launch_bounds__(64) void gen_region_kernel(GenParams p) {
         if (sl[k] >= 0) *reinterpret_cast<uint4*>(row + sl[k] * 16u) = tp[k];
     for (uint32_t j = 0; j < p.nf; j++) {  // fields in order (uniform)
         const GenField& f = p.f[j];
+        const GenFieldPlan& fp = p.plan[j];
         const uint64_t v = act ? field_value(f, i, g) : 0;
-        for (uint32_t k = f.s >> 7; k <= (f.e >> 7); k++) {
-            uint8_t* at = row + sl[k] * 16u;
+        for (uint32_t q = 0; q < fp.np; q++) {
+            const GenPut& pp = fp.p[q];
+            const int32_t sh = pp.sh;  // uniform: the branches below are scalar
+            U128 V;
+            if (sh >= 64) V = U128{v << (sh - 64), 0};
+            else if (sh > 0) V = U128{v >> (64 - sh), v << sh};
+            else if (sh == 0) V = U128{0, v};
+            else V = U128{0, v >> (-sh)};
+            uint8_t* at = row + pp.lds_off;
             U128 x = lds_get(at);
-            put_bits(x, f.s, f.e, f.w, v, k * 128u);
+            x.hi = (x.hi & ~pp.mhi) | (V.hi & pp.mhi);
+            x.lo = (x.lo & ~pp.mlo) | (V.lo & pp.mlo);
             lds_put(at, x);
         }
     }
     for (uint32_t c = 0; c < p.ncs; c++) {  // checksums last (uniform)
-        const uint32_t hb = p.csum_at[c], k0 = hb >> 4, r = hb & 15u;
-        const U128 x0 = lds_get(row + sl[k0] * 16u), x1 = lds_get(row + sl[k0 + 1] * 16u);
-        const U128 x2 = r + 20u > 32u ? lds_get(row + sl[k0 + 2] * 16u) : U128{0, 0};
+        // the header's 20 bytes lie contiguous in the row (its pieces are dirty, so their slots are
+        // consecutive): five unaligned dwords, the nine big-endian words but the checksum's (Q1 fold)
+        uint8_t* h = row + p.csum_lds[c];
+        uint32_t d[5];
+        __builtin_memcpy(d, h, 20);
         uint32_t sum = 0;
 #pragma unroll
-        for (uint32_t j = 0; j < 20; j += 2)
-            if (j != 10) sum += (byte3(x0, x1, x2, r + j) << 8) | byte3(x0, x1, x2, r + j + 1);
-        const uint32_t cv = ~(((sum >> 16) + sum) & 0xFFFFu) & 0xFFFFu;  // packet.rs:102-104 (Q1)
-        const uint32_t cb = hb + 10u;
-        for (uint32_t k = cb >> 4; k <= ((cb + 1u) >> 4); k++) {
-            uint8_t* at = row + sl[k] * 16u;
-            U128 x = lds_get(at);
-            put_bits(x, cb * 8u, cb * 8u + 15u, 16u, cv, k * 128u);
-            lds_put(at, x);
+        for (int k = 0; k < 5; k++) {
+            const uint32_t b = __builtin_bswap32(d[k]);
+            sum += (b >> 16) + (k == 2 ? 0u : (b & 0xFFFFu));  // bytes 10-11: the checksum itself
         }
+        const uint32_t cv = ~(((sum >> 16) + sum) & 0xFFFFu) & 0xFFFFu;  // packet.rs:102-104 (Q1)
+        h[10] = (uint8_t)(cv >> 8);
+        h[11] = (uint8_t)cv;
     }
     __syncthreads();
     const uint32_t npk = p.npkts - w0 < 64u ? p.npkts - w0 : 64u;
@@ -250,6 +278,11 @@ struct pkt_gen {
     uint32_t len = 0, tpl_bytes = 0;
     std::vector<GenField> fields;
     std::vector<uint32_t> csum_at;
+    // region-kernel placement (pieces < 64 only): slot per piece, dirty pieces, the field plans
+    int8_t slot[64];
+    uint32_t nd = 0;
+    bool region_ok = false;  // every touched piece < 64
+    GenFieldPlan* plan = nullptr;  // device, [fields]
 };
 
 extern "C" {
@@ -349,7 +382,48 @@ int pkt_gen_create(pkt_ctx_t* ctx, const uint8_t* tpl, uint32_t len, int entry, 
             G->csum_at.push_back((uint32_t)at);
         }
     }
+    if (rc == PKT_SUCCESS) {
+        // the region kernel's placement: the pieces a field or a checksum (its whole 20-byte header)
+        // touches get consecutive LDS slots, and each field's puts are precomputed
+        bool dirty[64] = {};
+        G->region_ok = true;
+        auto touch = [&](uint32_t k) {
+            if (k < 64) dirty[k] = true;
+            else G->region_ok = false;
+        };
+        for (const GenField& f : G->fields)
+            for (uint32_t k = f.s >> 7; k <= (f.e >> 7); k++) touch(k);
+        for (uint32_t at : G->csum_at)
+            for (uint32_t k = at >> 4; k <= ((at + 19u) >> 4); k++) touch(k);
+        G->nd = 0;
+        for (uint32_t k = 0; k < 64; k++) G->slot[k] = dirty[k] ? (int8_t)G->nd++ : (int8_t)-1;
+        std::vector<GenFieldPlan> plan(std::max<size_t>(1, G->fields.size()));
+        for (size_t j = 0; j < G->fields.size() && G->region_ok; j++) {
+            const GenField& f = G->fields[j];
+            GenFieldPlan& fp = plan[j];
+            std::memset(&fp, 0, sizeof(fp));
+            for (uint32_t k = f.s >> 7; k <= (f.e >> 7); k++) {
+                GenPut& pp = fp.p[fp.np++];
+                pp.lds_off = (uint32_t)G->slot[k] * 16u;
+                pp.sh = 127 - ((int32_t)f.e - (int32_t)(k * 128u));  // value bit 0 from the piece's LSB
+                // the field's bits within the piece: w ones shifted by sh (clipped to 128 bits)
+                const uint64_t ones = f.w >= 64 ? ~0ull : ((1ull << f.w) - 1ull);
+                uint64_t mhi = 0, mlo = 0;
+                const int32_t sh = pp.sh;
+                if (sh >= 64) mhi = sh - 64 < 64 ? ones << (sh - 64) : 0;
+                else if (sh > 0) mhi = ones >> (64 - sh), mlo = ones << sh;
+                else if (sh == 0) mlo = ones;
+                else mlo = -sh < 64 ? ones >> (-sh) : 0;
+                pp.mhi = mhi;
+                pp.mlo = mlo;
+            }
+        }
+        e = hipMalloc(reinterpret_cast<void**>(&G->plan), plan.size() * sizeof(GenFieldPlan));
+        if (e == hipSuccess) e = hipMemcpy(G->plan, plan.data(), plan.size() * sizeof(GenFieldPlan), hipMemcpyHostToDevice);
+        if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMalloc (generator plan)");
+    }
     if (rc != PKT_SUCCESS) {
+        if (G) (void)hipFree(G->plan);
         delete G;
         (void)hipFree(dtpl);
         return rc;
@@ -365,6 +439,7 @@ int pkt_gen_destroy(pkt_gen_t* g) {
         (void)hipSetDevice(g->ctx->device);
         (void)hipDeviceSynchronize();  // runs still in flight read the template
         (void)hipFree(g->tpl);
+        (void)hipFree(g->plan);
     }
     delete g;
     return PKT_SUCCESS;
@@ -391,15 +466,11 @@ int pkt_gen_run(pkt_gen_t* g, uint64_t first, uint64_t n, uint32_t stride, const
     p.nf = (uint32_t)g->fields.size();
     p.ncs = (uint32_t)g->csum_at.size();
     for (uint32_t c = 0; c < p.ncs; c++) p.csum_at[c] = g->csum_at[c];
-    // the pieces a field or a checksum (its whole 20-byte header) touches, for the region kernel
-    bool dirty[64] = {};
-    if (p.ppp <= 64) {
-        for (const GenField& f : g->fields)
-            for (uint32_t k = f.s >> 7; k <= (f.e >> 7) && k < 64; k++) dirty[k] = true;
-        for (uint32_t c = 0; c < p.ncs; c++)
-            for (uint32_t k = p.csum_at[c] >> 4; k <= ((p.csum_at[c] + 19u) >> 4) && k < 64; k++) dirty[k] = true;
-        for (uint32_t k = 0; k < 64; k++) p.slot[k] = (k < p.ppp && dirty[k]) ? (int8_t)p.nd++ : (int8_t)-1;
-    }
+    // the region kernel's placement (pkt_gen_create)
+    p.nd = g->nd;
+    for (uint32_t k = 0; k < 64; k++) p.slot[k] = k < p.ppp ? g->slot[k] : (int8_t)-1;
+    for (uint32_t c = 0; c < p.ncs; c++) p.csum_lds[c] = (uint32_t)g->slot[p.csum_at[c] >> 4] * 16u + (p.csum_at[c] & 15u);
+    p.plan = g->plan;
     p.pk_magic = ((1u << 20) + p.ppp - 1) / p.ppp;
     const uint64_t per = std::max<uint64_t>(1, kGenChunkPieces / p.ppp);  // packets per launch
     for (uint64_t i0 = 0; i0 < n; i0 += per) {
@@ -414,7 +485,7 @@ int pkt_gen_run(pkt_gen_t* g, uint64_t first, uint64_t n, uint32_t stride, const
         p.npkts = (uint32_t)m;
         // region kernel whenever a field or checksum is applied and the 64-packet region fits LDS;
         // pure clones (and strides over 1 KiB) take the lane-per-piece kernel
-        if ((p.nf || p.ncs) && stride <= kRegionMaxStride)
+        if ((p.nf || p.ncs) && stride <= kRegionMaxStride && g->region_ok)
             hipLaunchKernelGGL(gen_region_kernel, dim3((p.npkts + 63) / 64), dim3(64), 64u * 16u * p.nd,
                                reinterpret_cast<hipStream_t>(stream), p);
         else

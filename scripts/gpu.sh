@@ -22,6 +22,7 @@
 #   ab=CFGS:VARS       every lib/variants/*.so through kbench, interleaved (scripts/ab.sh)
 #   abn=CFG:VARS:A,B   named builds (main = lib/libpktgpu.so, else lib/variants/NAME.so), kbench, 3 rounds
 #   pcapn=A,B          named builds through scripts/pcap_index_bench.py, 3 interleaved rounds
+#   secn=W1,W2:A,B     named builds through scripts/secondary_bench.py --only W1,W2, 3 interleaved rounds
 set -u
 TAG=$1; shift
 OUT=gpurun_out/$TAG; mkdir -p "$OUT"
@@ -73,6 +74,9 @@ for step in "$@"; do
                python scripts/hostpath_native.py --config $c --pageable --chunks 131072,262144 || exit $?; done' ;;
     ab)    IFS=: read -r c v <<< "$arg"; run ab_${c:-c2} 900 bash scripts/ab.sh "${c:-c2}" "${v:-status;chain;all}" 2 ;;
     abn)   IFS=: read -r c v names <<< "$arg"; run abn_${c}_$(echo "${v:-all}" | tr -c 'a-z0-9' '_') 900 bash scripts/ab_named.sh "$c" "${v:-all}" 3 ${names//,/ } ;;
+    secn)  IFS=: read -r only names <<< "$arg"; run secn_$(echo "$only" | tr -c 'a-z0-9' '_') 900 bash -c 'for rep in 1 2 3; do for name in '"${names//,/ }"'; do
+               lib=packet-rs_amd/lib/variants/$name.so; [ "$name" = main ] && lib=packet-rs_amd/lib/libpktgpu.so
+               PKTGPU_LIB=$lib timeout -k 10 300 python scripts/secondary_bench.py --only '"$only"' --cpu-budget 0.02 | sed "s|^|$name |" || exit $?; done; done' ;;
     pcapn) IFS=: read -r names <<< "$arg"; run pcapn 600 bash -c 'for rep in 1 2 3; do for name in '"${names//,/ }"'; do
                lib=packet-rs_amd/lib/variants/$name.so; [ "$name" = main ] && lib=packet-rs_amd/lib/libpktgpu.so
                PKTGPU_LIB=$lib timeout -k 10 120 python scripts/pcap_index_bench.py --reps 20 | sed "s|^|$name |" || exit $?; done; done' ;;
