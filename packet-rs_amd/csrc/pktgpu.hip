@@ -313,9 +313,11 @@ __device__ __forceinline__ const DispatchLds* tables(uint8_t* lds, size_t at, ui
 // was measured no faster at k = 4 and slower at k = 1, 2: DESIGN.md §5.)
 // Resident waves per SIMD the compiler may assume (VGPR budget 512 / waves): 8 for fixed-stride
 // windows (<= 64 VGPRs); for indexed windows what their LDS allows anyway — 6 for the 96-byte
-// windows (25.6 KB per block, 6 blocks per CU), 4 for the 144-byte ones (37.9 KB, 4 blocks); wider
-// windows unconstrained.
-__host__ __device__ constexpr int waves_per_eu(int nch, int wk) { return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : 6) : 8); }
+// windows (25.6 KB per block, 6 blocks per CU), 5 for the 112-byte ones (29.7 KB, 5 blocks), 4 for
+// the 144-byte ones (37.9 KB, 4 blocks); wider windows unconstrained.
+__host__ __device__ constexpr int waves_per_eu(int nch, int wk) {
+    return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : nch == 7 ? 5 : 6) : 8);
+}
 // Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
 template <int NCH, uint32_t GM, int WK, bool LATE = false>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
@@ -676,9 +678,9 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiPa
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
 hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s, const MultiParams* mp) {
-    // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 9 and
-    // 17 chunks only (parse_impl widens a narrower request)
-    if constexpr (NCH >= 6 && NCH != 7) if (wk == 1) {
+    // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 7, 9
+    // and 17 chunks only (window requests of <= 80, 96, 128 and 256 B; parse_impl widens the rest)
+    if constexpr (NCH >= 6) if (wk == 1) {
         switch (gm) {
             case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp);
             case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp);
@@ -1064,6 +1066,7 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         else if (nch <= 4) e = launch_gm<4>(kp, gm, md, wk, s, mp);
         else if (nch <= 5) e = launch_gm<5>(kp, gm, md, wk, s, mp);
         else if (nch <= 6) e = launch_gm<6>(kp, gm, md, wk, s, mp);
+        else if (nch <= 7 && wk == 1) e = launch_gm<7>(kp, gm, md, wk, s, mp);
         else if (nch <= 9) e = launch_gm<9>(kp, gm, md, wk, s, mp);
         else e = launch_gm<17>(kp, gm, md, wk, s, mp);
     }

@@ -44,7 +44,10 @@
 
 namespace {
 
-constexpr uint32_t kRegion = 4096;                // bytes of record starts per region
+#ifndef PKTGPU_PCAP_REGION
+#define PKTGPU_PCAP_REGION 4096
+#endif
+constexpr uint32_t kRegion = PKTGPU_PCAP_REGION;  // bytes of record starts per region
 static_assert(kRegion % 16 == 0 && kRegion / 16 <= 65536, "u16 record lists");
 constexpr uint32_t kMaxRec = kRegion / 16;       // records per region (each >= 16 B apart)
 constexpr int kWaves = 4;                         // waves (regions) per 256-thread block
@@ -301,6 +304,9 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
 
 // Region k's guessed entry (the candidate scan of the staged tile at lbase); base + kRegion =
 // "no record starts here".
+#ifndef PKTGPU_PCAP_STEPS
+#define PKTGPU_PCAP_STEPS 1
+#endif
 template <uint32_t STAGED>
 __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf, uint64_t len, const uint32_t* lw,
                                                 uint64_t lbase, uint32_t k) {
@@ -312,6 +318,27 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
     if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
     const uint64_t stop = len < base + kRegion ? len : base + kRegion;
     const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
+    if constexpr (PKTGPU_PCAP_STEPS > 1) {
+        // PKTGPU_PCAP_STEPS candidate steps per pass: lane l checks candidates c0 + 64 j + l, all
+        // their LDS reads in flight together; step j's verdict is then taken exactly as the one-step
+        // loop below would (lowest locally verified candidate of the step, else the global re-check)
+        for (uint64_t c0 = base; c0 < stop; c0 += 64 * PKTGPU_PCAP_STEPS) {
+            int r[PKTGPU_PCAP_STEPS];
+#pragma unroll
+            for (int j = 0; j < PKTGPU_PCAP_STEPS; j++) {
+                const uint64_t c = c0 + 64 * j + lane;
+                r[j] = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
+            }
+#pragma unroll
+            for (int j = 0; j < PKTGPU_PCAP_STEPS; j++) {
+                const uint64_t c = c0 + 64 * j + lane;
+                uint64_t m = __ballot(r[j] == 1);
+                if (!m) m = __ballot(r[j] == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
+                if (m) return c0 + 64 * j + (uint64_t)__builtin_ctzll(m);
+            }
+        }
+        return base + kRegion;
+    }
     for (uint64_t c0 = base; c0 < stop; c0 += 64) {
         // The lowest candidate whose chain checks out inside the staged bytes wins; only when
         // there is none do the candidates whose chains leave them read global memory.
@@ -379,6 +406,57 @@ __device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, ui
     cnt = c | (e ? 0x80000000u : 0u);
 }
 
+// lane_walk without branches (PKTGPU_PCAP_WALK2): the walking lanes run a loop whose trip count is
+// uniform (until no lane is active, two hops per test); a finished lane reads a safe LDS address and
+// stores its would-be offset to a dummy slot (lst[kMaxRec]), so a hop is one ds_read2, the
+// arithmetic and one ds_write with no exec-mask save/restore (the branchy loop above spent ~25
+// scalar and vector instructions per hop on them, ~380 cycles per hop in the guess kernel's
+// stamps: profiles/pcap/r04m_stamps.txt).  `valid` = the lane has a region to walk.
+#ifndef PKTGPU_PCAP_WALK2
+#define PKTGPU_PCAP_WALK2 1
+#endif
+// The walks store the record offsets straight into the regions' lists in global memory instead of
+// an LDS list copied out afterwards (2 KiB less LDS per block).
+#ifndef PKTGPU_PCAP_GLIST
+#define PKTGPU_PCAP_GLIST 0
+#endif
+
+__device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, uint16_t* lst, uint64_t base, uint64_t entry,
+                                           uint64_t len, bool valid, uint64_t& exit, uint32_t& cnt) {
+    const uint32_t rb = (uint32_t)(base - lbase);
+    const uint32_t room = valid ? (uint32_t)(len - lbase) - rb : 0u;  // < 2^31 (the caller checks)
+    const uint32_t lim = room >= 16 ? (room - 15 < kRegion ? room - 15 : kRegion) : 0u;
+    const uint8_t* lb = reinterpret_cast<const uint8_t*>(lw) + rb;
+    // q walks freely (a finished lane's hops are never recorded; min(q, kRegion) keeps its reads
+    // inside the staged bytes), qe holds the exit: the chain from one read to the next is a min,
+    // an add3 and a min3
+    uint32_t q = (!valid || entry >= base + kRegion) ? kRegion : (uint32_t)(entry - base), qe = q, c = 0, e = 0;
+    bool act = q < lim;
+    auto hop = [&]() {
+        uint32_t incl;
+        __builtin_memcpy(&incl, lb + __builtin_elementwise_min(q, kRegion) + 8, 4);  // unaligned LDS read
+        const uint32_t t = q + 16 + __builtin_elementwise_min(incl, room);            // < 2^32
+        const bool over = act & (t > room);  // pkt_pcap_index: record runs past the end
+        const bool rec = act & !over;
+        if constexpr (PKTGPU_PCAP_GLIST) {
+            if (rec) lst[c] = (uint16_t)q;  // straight to the region's list in global memory
+        } else {
+            lst[rec ? c : kMaxRec] = (uint16_t)q;
+        }
+        c += rec ? 1u : 0u;
+        e |= over ? 1u : 0u;
+        q = __builtin_elementwise_min(t, room);
+        qe = act ? q : qe;
+        act = rec & (q < lim);
+    };
+    while (__ballot(act)) {
+        hop();
+        hop();
+    }
+    exit = base + qe;
+    cnt = c | (e ? 0x80000000u : 0u);
+}
+
 // GUESS (file header): one region per wave, a block stages 4 consecutive regions (16 KiB + 16 B).
 // (One wave per 8 KiB tile walking its second region on from the first's exit — half the candidate
 // scans — measured slower: 77 vs 63 us per 2^20-record call; the kernel is bound by each wave's
@@ -390,37 +468,75 @@ __device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, ui
 #ifndef PKTGPU_PCAP_LANEWALK
 #define PKTGPU_PCAP_LANEWALK 1
 #endif
+// Diagnostic build only (-DPKTGPU_STAMPS=1, read by scripts/pcap_stamps.py): per wave of the guess
+// kernel, s_memrealtime at the start, after the staging barrier, after its candidate scan, after the
+// walk barrier and after its stores drained, + XCC id and the entry's distance from the region
+// base, written by lane 0 to a debug buffer nothing else reads (pkt_debug_pcap_stamps).
+#ifndef PKTGPU_STAMPS
+#define PKTGPU_STAMPS 0
+#endif
+#if PKTGPU_STAMPS
+__device__ uint64_t* g_pcap_stamps;
+#define PCAP_STAMP(k)                                                               \
+    do {                                                                            \
+        __builtin_amdgcn_sched_barrier(0);                                          \
+        uint64_t t_;                                                                \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        __builtin_amdgcn_sched_barrier(0);                                          \
+        st_[k] = t_;                                                                \
+    } while (0)
+#else
+#define PCAP_STAMP(k) \
+    do {              \
+    } while (0)
+#endif
 __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                          Scratch S) {
     constexpr uint32_t kStaged = kWaves * kRegion;
     __shared__ uint4 lds[kStaged / 16 + 2];
-    __shared__ uint16_t lst[kWaves][kMaxRec];
+    constexpr uint32_t kLst = PKTGPU_PCAP_GLIST ? 1 : kMaxRec + 2;  // + the dummy slot of lane_walk2
+    __shared__ uint16_t lst[kWaves][kLst];
     __shared__ uint64_t s_entry[kWaves], s_exit[kWaves];
     __shared__ uint32_t s_cnt[kWaves];
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     const uint64_t lbase = (uint64_t)blockIdx.x * kStaged;
+#if PKTGPU_STAMPS
+    uint64_t st_[5] = {0, 0, 0, 0, 0};
+#endif
+    PCAP_STAMP(0);
     stage<kStaged, 256>(lds, buf, lbase, len, t);
     __syncthreads();
+    PCAP_STAMP(1);
     const uint32_t k = blockIdx.x * kWaves + w;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     const uint64_t base = (uint64_t)k * kRegion;
     if (PKTGPU_PCAP_LANEWALK && len - lbase <= 0xFFFFFFF0ull) {
+        // (lane_walk2 needs the file's end < 2 GiB past the staged bytes; lane_walk takes the rest)
+        const bool w2 = PKTGPU_PCAP_WALK2 && len - lbase <= 0x7FFFFFF0ull;
         const uint64_t entry = k >= K ? base + kRegion : (k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k));
+        PCAP_STAMP(2);
         if (lane == 0) s_entry[w] = entry;
         __syncthreads();
         if (w == 0 && lane < (uint32_t)kWaves) {
             const uint32_t kk = blockIdx.x * kWaves + lane;
             uint64_t ex = 0;
             uint32_t cw = 0;
-            if (kk < K) lane_walk(lw, lbase, lst[lane], (uint64_t)kk * kRegion, s_entry[lane], len, ex, cw);
+            uint16_t* ll = PKTGPU_PCAP_GLIST ? S.list + (uint64_t)kk * kMaxRec : lst[lane];
+            if (w2)
+                lane_walk2(lw, lbase, ll, (uint64_t)kk * kRegion, s_entry[lane], len, kk < K, ex, cw);
+            else if (kk < K)
+                lane_walk(lw, lbase, ll, (uint64_t)kk * kRegion, s_entry[lane], len, ex, cw);
             s_exit[lane] = ex;
             s_cnt[lane] = cw;
         }
         __syncthreads();
+        PCAP_STAMP(3);
         if (k >= K) return;
         const uint32_t cw = s_cnt[w], cnt = cw & 0x7FFFFFFFu;
-        uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
-        for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
+        if constexpr (!PKTGPU_PCAP_GLIST) {
+            uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+            for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
+        }
         if (lane == 0) {
             S.rentry[k] = entry;
             S.rexit[k] = s_exit[w];
@@ -431,6 +547,19 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
                 S.dev[1] = mg;
             }
         }
+#if PKTGPU_STAMPS
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        PCAP_STAMP(4);
+        if (lane == 0 && g_pcap_stamps) {
+            uint32_t xcc;
+            asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+            uint64_t* d = g_pcap_stamps + (uint64_t)k * 8u;
+            for (int q = 0; q < 5; q++) d[q] = st_[q];
+            d[5] = xcc & 15u;
+            d[6] = entry - base;
+            d[7] = cw & 0x7FFFFFFFu;
+        }
+#endif
         return;
     }
     if (k >= K) return;
@@ -443,11 +572,12 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     // (the walk reading each incl_len by scalar-unit loads from L2 instead of LDS halves the VALU
     // instructions, 736 -> 374 per wave, but each hop then waits ~3x longer: 80 vs 63 us per call,
     // profiles/ab/r03i_pcap_uniform_walk.txt)
-    walk(lw, lbase, lst[w], base, entry, len, exit, cnt, err, rec);
-    wave_lds_sync();
     uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+    walk(lw, lbase, PKTGPU_PCAP_GLIST ? dst : lst[w], base, entry, len, exit, cnt, err, rec);
+    wave_lds_sync();
     if (lane < cnt) dst[lane] = (uint16_t)rec;
-    for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = lst[w][i];
+    if constexpr (!PKTGPU_PCAP_GLIST)
+        for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = lst[w][i];
     if (lane == 0) {
         S.rentry[k] = entry;
         S.rexit[k] = exit;
@@ -892,6 +1022,14 @@ static int pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) {
 }
 
 extern "C" {
+
+#if PKTGPU_STAMPS
+// Diagnostic build only: where the guess kernel writes its per-wave stamps (8 u64 per region).
+int pkt_debug_pcap_stamps(void* dev_buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pcap_stamps), &dev_buf, sizeof(dev_buf)) == hipSuccess ? PKT_SUCCESS
+                                                                                            : PKT_ERR_HIP;
+}
+#endif
 
 int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                           uint64_t cap, uint64_t* n_out, void* stream) {

@@ -56,14 +56,15 @@ for step in "$@"; do
            run kbench_${c}_st${st:-0} 300 python scripts/kbench.py --config $c --variants "${v:-status;chain;all}" --windows ${w:-0} \
                --staging ${st:-0} --streams 1,2 --rounds 3 --iters 24 ;;
     anat)  run anat_${arg:-c4} 900 bash scripts/gpu_c4anat.sh ${TAG}_anat ;;
-    sq)    IFS=: read -r c v <<< "$arg"; n=sq_${c}_$(echo "${v:-all}" | tr -c 'a-z0-9' '_')
-           run $n 600 bash scripts/pmc.sh ${TAG}_$n "${v:-all}" $c
+    sq)    IFS=: read -r c v w <<< "$arg"; n=sq_${c}_$(echo "${v:-all}${w:+_w$w}" | tr -c 'a-z0-9' '_')
+           run $n 600 bash scripts/pmc.sh ${TAG}_$n "${v:-all}" $c "--windows ${w:-0}"
            python scripts/pmc_summary.py gpurun_out/${TAG}_$n > "$OUT/$n.txt"; cat "$OUT/$n.txt" ;;
     stamps) run stamps 600 bash -c 'export PKTGPU_LIB=packet-rs_amd/lib/variants/stamps.so;
                for s in "c4 all 64" "c4 all 128"; do
                  set -- $s; python scripts/stamps.py --config $1 --columns $2 --window $3 || exit $?; done' ;;
     pcapab) run pcapab 900 bash -c 'for rep in 1 2 3; do for v in packet-rs_amd/lib/variants/*.so; do
                PKTGPU_LIB=$v python scripts/pcap_index_bench.py --reps 20 | sed "s|^|$(basename $v) |" || exit $?; done; done' ;;
+    pcapstamps) run pcapstamps 300 env PKTGPU_LIB=packet-rs_amd/lib/variants/stamps.so python scripts/pcap_stamps.py ;;
     pcap)  run pcap 300 python scripts/pcap_index_bench.py --reps 20
            run pcap_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/pcap_prof" -o trace -- \
                python scripts/pcap_index_bench.py --reps 10 ;;

@@ -620,6 +620,14 @@ def test_staging_modes_bit_exact(P, staging):
         P.set_window(0)
 
 
+@pytest.mark.parametrize("window", [80, 96, 112, 144])
+def test_lockstep_window_widths(P, window):
+    """The lockstep walk is compiled for 6, 7, 9 and 17 chunks (window requests up to 80, 96,
+    128 and 256 B); 112 and 144 are widened to 9 and 17 chunks: every width is bit-exact on C4."""
+    buf, offs, lens = gen.gen_c4(20011, seed=window)
+    both(P, buf, len(offs), offsets=offs, lens=lens, window=window, label=f"c4 w{window}")
+
+
 @pytest.mark.parametrize("staging", [0, 2])
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 65537])
 def test_indexed_sizes_and_wide_ranges(P, n, staging):
