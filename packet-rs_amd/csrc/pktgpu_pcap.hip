@@ -74,6 +74,8 @@ constexpr uint64_t kValMask = (1ull << (64 - kEpochBits)) - 1;
 __host__ __device__ constexpr uint64_t tagged(uint32_t epoch, uint64_t v) { return ((uint64_t)epoch << (64 - kEpochBits)) | v; }
 __host__ __device__ constexpr uint32_t tag_of(uint64_t w) { return (uint32_t)(w >> (64 - kEpochBits)); }
 enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4 };
+// a region's count word: records | kCntErr (the walk met a record running past the end)
+constexpr uint32_t kCntErr = 0x80000000u, kCntMask = 0x7FFFFFFFu;
 
 constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
 constexpr uint32_t kEmitRegions = 16;   // regions per emit block
@@ -304,9 +306,6 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
 
 // Region k's guessed entry (the candidate scan of the staged tile at lbase); base + kRegion =
 // "no record starts here".
-#ifndef PKTGPU_PCAP_STEPS
-#define PKTGPU_PCAP_STEPS 1
-#endif
 template <uint32_t STAGED>
 __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf, uint64_t len, const uint32_t* lw,
                                                 uint64_t lbase, uint32_t k) {
@@ -318,27 +317,6 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
     if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
     const uint64_t stop = len < base + kRegion ? len : base + kRegion;
     const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
-    if constexpr (PKTGPU_PCAP_STEPS > 1) {
-        // PKTGPU_PCAP_STEPS candidate steps per pass: lane l checks candidates c0 + 64 j + l, all
-        // their LDS reads in flight together; step j's verdict is then taken exactly as the one-step
-        // loop below would (lowest locally verified candidate of the step, else the global re-check)
-        for (uint64_t c0 = base; c0 < stop; c0 += 64 * PKTGPU_PCAP_STEPS) {
-            int r[PKTGPU_PCAP_STEPS];
-#pragma unroll
-            for (int j = 0; j < PKTGPU_PCAP_STEPS; j++) {
-                const uint64_t c = c0 + 64 * j + lane;
-                r[j] = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
-            }
-#pragma unroll
-            for (int j = 0; j < PKTGPU_PCAP_STEPS; j++) {
-                const uint64_t c = c0 + 64 * j + lane;
-                uint64_t m = __ballot(r[j] == 1);
-                if (!m) m = __ballot(r[j] == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
-                if (m) return c0 + 64 * j + (uint64_t)__builtin_ctzll(m);
-            }
-        }
-        return base + kRegion;
-    }
     for (uint64_t c0 = base; c0 < stop; c0 += 64) {
         // The lowest candidate whose chain checks out inside the staged bytes wins; only when
         // there is none do the candidates whose chains leave them read global memory.
@@ -377,7 +355,7 @@ __device__ __forceinline__ Agg region_agg(uint32_t k, uint32_t K, uint64_t entry
     if (k >= K) return agg_identity();
     const uint64_t end = ((uint64_t)k + 1) * kRegion;
     if (k != 0 && entry >= end) return Agg{0, end, 0, kBitNone};
-    return Agg{entry, exit, cw & 0x7FFFFFFFu, (cw >> 31) ? kBitErr : 0u};
+    return Agg{entry, exit, cw & kCntMask, (cw & kCntErr) ? kBitErr : 0u};
 }
 
 // The walk of one region by ONE lane (pcap_guess_kernel): pkt_pcap_index's loop from `entry` while the
@@ -403,7 +381,7 @@ __device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, ui
         q += 16 + incl;
     }
     exit = base + q;
-    cnt = c | (e ? 0x80000000u : 0u);
+    cnt = c | (e ? kCntErr : 0u);
 }
 
 // lane_walk without branches (PKTGPU_PCAP_WALK2): the walking lanes run a loop whose trip count is
@@ -454,7 +432,7 @@ __device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, u
         hop();
     }
     exit = base + qe;
-    cnt = c | (e ? 0x80000000u : 0u);
+    cnt = c | (e ? kCntErr : 0u);
 }
 
 // GUESS (file header): one region per wave, a block stages 4 consecutive regions (16 KiB + 16 B).
@@ -519,20 +497,21 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         __syncthreads();
         if (w == 0 && lane < (uint32_t)kWaves) {
             const uint32_t kk = blockIdx.x * kWaves + lane;
+            const uint64_t en = s_entry[lane];
             uint64_t ex = 0;
             uint32_t cw = 0;
             uint16_t* ll = PKTGPU_PCAP_GLIST ? S.list + (uint64_t)kk * kMaxRec : lst[lane];
             if (w2)
-                lane_walk2(lw, lbase, ll, (uint64_t)kk * kRegion, s_entry[lane], len, kk < K, ex, cw);
+                lane_walk2(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, kk < K, ex, cw);
             else if (kk < K)
-                lane_walk(lw, lbase, ll, (uint64_t)kk * kRegion, s_entry[lane], len, ex, cw);
+                lane_walk(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, ex, cw);
             s_exit[lane] = ex;
             s_cnt[lane] = cw;
         }
         __syncthreads();
         PCAP_STAMP(3);
         if (k >= K) return;
-        const uint32_t cw = s_cnt[w], cnt = cw & 0x7FFFFFFFu;
+        const uint32_t cw = s_cnt[w], cnt = cw & kCntMask;
         if constexpr (!PKTGPU_PCAP_GLIST) {
             uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
             for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
@@ -557,7 +536,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             for (int q = 0; q < 5; q++) d[q] = st_[q];
             d[5] = xcc & 15u;
             d[6] = entry - base;
-            d[7] = cw & 0x7FFFFFFFu;
+            d[7] = cw & kCntMask;
         }
 #endif
         return;
@@ -581,7 +560,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     if (lane == 0) {
         S.rentry[k] = entry;
         S.rexit[k] = exit;
-        S.rcnt[k] = cnt | (err ? 0x80000000u : 0u);
+        S.rcnt[k] = cnt | (err ? kCntErr : 0u);
         if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
             const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
             __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -644,11 +623,17 @@ __device__ __forceinline__ bool seam_bad(const Agg& pre, const Agg& r) {
     return (r.bits & kBitNone) ? pre.last < r.last : pre.last != r.first;
 }
 
+#ifndef PKTGPU_PCAP_FIXWALK2
+#define PKTGPU_PCAP_FIXWALK2 1
+#endif
+#ifndef PKTGPU_PCAP_REUSE
+#define PKTGPU_PCAP_REUSE 1
+#endif
 // Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
 __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                         uint32_t nb, int ticket, Scratch S) {
     __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
-    __shared__ uint16_t lst[kWaves][kMaxRec];
+    __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
     __shared__ uint64_t sen[kScanRegions], sex[kScanRegions];
     __shared__ uint32_t scw[kScanRegions];
     __shared__ uint32_t fq[kScanRegions];
@@ -659,6 +644,11 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     __shared__ uint32_t s_blk, s_nf, s_retry, s_near, csum[kWaves];
     __shared__ Agg s_P;
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
+#if PKTGPU_STAMPS
+    uint64_t st_[5] = {0, 0, 0, 0, 0};
+    uint32_t n_fix = 0, n_wait = 0;
+#endif
+    PCAP_STAMP(0);
     // the block order: blockIdx when every block of the grid is resident at once (the host checks
     // the occupancy), else a ticket (every lower block is then already running)
     if (t == 0) s_blk = ticket ? atomicAdd(S.ticket, 1u) : blockIdx.x;
@@ -674,6 +664,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         scw[t] = 0;
     }
     __syncthreads();
+    PCAP_STAMP(1);
     // Re-walk the queued regions fq[0, s_nf) from fe[]: one wave per region (stage its 4 KiB, walk),
     // the state to LDS and global memory.
     auto run_fixes = [&]() {
@@ -684,6 +675,30 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             wave_lds_sync();
             if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane);
             wave_lds_sync();
+            if (PKTGPU_PCAP_FIXWALK2 && len - base <= 0x7FFFFFF0ull) {  // wave-uniform
+                // one lane walks (lane_walk2: the whole-wave walk below took ~9 us per fixed
+                // region, on the scan's critical path: profiles/pcap/r04q_stamps_guess_scan.txt)
+                uint64_t ex = 0;
+                uint32_t cw = 0;
+                if (lane == 0)
+                    lane_walk2(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, true, ex, cw);
+                wave_lds_sync();
+                cw = (uint32_t)__shfl((int)cw, 0, 64);
+                ex = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex >> 32), 0, 64) << 32) |
+                     (uint32_t)__shfl((int)(uint32_t)ex, 0, 64);
+                const uint32_t cnt = cw & kCntMask;
+                uint16_t* dst = S.list + (uint64_t)kk * kMaxRec;
+                for (uint32_t j = lane; j < cnt; j += 64) dst[j] = lst[w][j];
+                if (lane == 0) {
+                    sen[r] = e;
+                    sex[r] = ex;
+                    scw[r] = cw;
+                    S.rentry[kk] = e;
+                    S.rexit[kk] = ex;
+                    S.rcnt[kk] = cw;
+                }
+                continue;
+            }
             uint64_t exit;
             uint32_t cnt, err, rec;
             walk(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, exit, cnt, err, rec);
@@ -692,7 +707,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             if (lane < cnt) dst[lane] = (uint16_t)rec;
             for (uint32_t j = 64 + lane; j < cnt; j += 64) dst[j] = lst[w][j];
             if (lane == 0) {
-                const uint32_t cw = cnt | (err ? 0x80000000u : 0u);
+                const uint32_t cw = cnt | (err ? kCntErr : 0u);
                 sen[r] = e;
                 sex[r] = exit;
                 scw[r] = cw;
@@ -705,11 +720,12 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     };
     // ---- local fixes: a region that disagrees with the claiming region before it (in this block)
     // while that one agrees with its own left is re-walked from its exit; until no such region
-    Agg total;
+    Agg total, pre_cur;  // pre_cur: the block-exclusive composition of the current states
     for (;;) {
         const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
         int32_t j;
         const Agg pre = block_exclusive(mine, j, wtot, widx, total);
+        pre_cur = pre;
         const bool bad = j >= 0 && seam_bad(pre, mine);
         sbad[t] = bad;
         // (an exit landing before this region's start means a "none" region between is wrong: that
@@ -723,8 +739,12 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         __syncthreads();
         if (s_nf == 0) break;
+#if PKTGPU_STAMPS
+        n_fix += s_nf;
+#endif
         run_fixes();
     }
+    PCAP_STAMP(2);
     // ---- publish the aggregate; compose the blocks before (stopping at the nearest exact one)
     BlkDesc* my = S.blk + blk;
     if (t == 0) {
@@ -809,6 +829,9 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         __syncthreads();
         if (s_retry || !exact) {  // a block before has not published, or none is exact yet
+#if PKTGPU_STAMPS
+            n_wait++;
+#endif
             __builtin_amdgcn_s_sleep(8);
             continue;
         }
@@ -826,15 +849,24 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             P = Agg{0, acc.last, ic + acc.cnt, ib | (acc.bits & kBitErr)};
             break;
         }
+#if PKTGPU_STAMPS
+        n_wait += 1u << 16;
+#endif
         __builtin_amdgcn_s_sleep(8);  // an earlier block has not fixed its first seam yet
     }
+    PCAP_STAMP(3);
     // ---- this block's seams against the exact exit before it: fix the first disagreeing region
     // from the exact state before it, until none disagrees (exact by induction)
     Agg exact_pre = blk == 0 ? agg_identity() : Agg{P.last, P.last, 0, 0};  // "claims" the exact exit
-    for (;;) {
+    // (the states have not changed since the local fixes' last composition: reuse it, and recompose
+    // only after a fix below)
+    for (bool fresh = PKTGPU_PCAP_REUSE != 0;; fresh = false) {
         const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
-        int32_t j;
-        const Agg pre0 = block_exclusive(mine, j, wtot, widx, total);
+        if (!fresh) {
+            int32_t j;
+            pre_cur = block_exclusive(mine, j, wtot, widx, total);
+        }
+        const Agg pre0 = pre_cur;
         const Agg pre = combine(exact_pre, pre0);
         const bool bad = seam_bad(pre, mine) && !(pre.bits & kBitBad) && pre.last >= (uint64_t)k * kRegion;
         if (t == 0) s_nf = 0;
@@ -846,6 +878,9 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         __syncthreads();
         if (s_nf == 0) break;
+#if PKTGPU_STAMPS
+        n_fix += s_nf;
+#endif
         run_fixes();
     }
     // ---- the exact state after this block; each region's record prefix
@@ -869,9 +904,12 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
     }
-    // each region's exact record prefix (the emit kernel writes the records)
-    {
-        uint32_t x = k < K ? (scw[t] & 0x7FFFFFFFu) : 0u, c = x;
+    // each region's exact record prefix (the emit kernel writes the records): the records of the
+    // regions before it in the block are the exclusive composition's count
+    if (PKTGPU_PCAP_REUSE) {
+        if (k < K) S.rpre[k] = c_before + pre_cur.cnt;
+    } else {
+        uint32_t x = k < K ? (scw[t] & kCntMask) : 0u, c = x;
 #pragma unroll
         for (uint32_t d = 1; d < 64; d <<= 1) {
             const uint32_t y = __shfl_up(x, d, 64);
@@ -883,6 +921,17 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         for (uint32_t q = 0; q < w; q++) before += csum[q];
         if (k < K) S.rpre[k] = before + x - c;
     }
+#if PKTGPU_STAMPS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    PCAP_STAMP(4);
+    if (t == 0 && g_pcap_stamps) {  // after the guess kernel's K rows: one row per scan block
+        uint64_t* d = g_pcap_stamps + ((uint64_t)K + blk) * 8u;
+        for (int q = 0; q < 5; q++) d[q] = st_[q];
+        d[5] = n_fix;
+        d[6] = n_wait;
+        d[7] = blk;
+    }
+#endif
 }
 
 // Emit (file header: EMIT): 256 threads write the records of 16 consecutive regions, one record per
@@ -893,7 +942,7 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
     __shared__ uint32_t cpre[kEmitRegions + 1];
     const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
     if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
-        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & 0x7FFFFFFFu) : 0;
+        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & kCntMask) : 0;
         uint32_t x = c;
 #pragma unroll
         for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {

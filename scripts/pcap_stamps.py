@@ -36,7 +36,8 @@ def call():
 for _ in range(3):
     call()
 K = (buf.size + 4095) // 4096
-st = torch.zeros(K * 8, dtype=torch.uint64, device="cuda")
+NB = (K + 255) // 256
+st = torch.zeros((K + NB) * 8, dtype=torch.uint64, device="cuda")
 D = ctypes.CDLL(os.environ["PKTGPU_LIB"])
 D.pkt_debug_pcap_stamps.argtypes = [ctypes.c_void_p]
 assert D.pkt_debug_pcap_stamps(ctypes.c_void_p(st.data_ptr())) == 0
@@ -45,9 +46,12 @@ call()
 torch.cuda.synchronize()
 D.pkt_debug_pcap_stamps(ctypes.c_void_p(0))
 assert cnt.value == n and np.array_equal(o.cpu().numpy(), offs)
-x = st.cpu().numpy().view(np.int64).reshape(K, 8)
+xa = st.cpu().numpy().view(np.int64).reshape(K + NB, 8)
+y = xa[K:].copy()
+x = xa[:K]
 x = x[x[:, 0] != 0].copy()
-x[:, :5] -= x[:, 0].min()  # one device-wide constant clock
+t00 = x[:, 0].min()
+x[:, :5] -= t00  # one device-wide constant clock
 span = x[:, 4].max()
 # s_memrealtime: the 100 MHz constant clock -> us
 f = 100.0
@@ -67,3 +71,17 @@ steps = dist // 64 + 1
 for q in (1, 2, 3, 4, 5):
     print(f"    candidate steps == {q}: {(steps == q).mean():6.1%}")
 print(f"    candidate steps > 5: {(steps > 5).mean():6.1%}")
+
+# scan blocks (one row per block: start, states loaded, local fixes done, look-back done, end)
+y = y[y[:, 0] != 0]
+y[:, :5] -= t00
+print(f"scan: {len(y)} blocks; first start {y[:, 0].min() / f:.1f} us after the first guess wave, "
+      f"last end {y[:, 4].max() / f:.1f} us")
+ss = {"states loaded": y[:, 1] - y[:, 0], "local fixes": y[:, 2] - y[:, 1], "look-back": y[:, 3] - y[:, 2],
+      "exact state + prefixes": y[:, 4] - y[:, 3], "block total": y[:, 4] - y[:, 0]}
+for k, v in ss.items():
+    print(f"  {k:28s} median {np.median(v) / f:7.2f} us  p90 {np.percentile(v, 90) / f:7.2f} us  max {v.max() / f:7.2f} us")
+print(f"  blocks with fixes: {(y[:, 5] > 0).sum()} (regions re-walked {y[:, 5].sum()}); look-back retries "
+      f"median {np.median(y[:, 6] & 0xFFFF):.0f} max {(y[:, 6] & 0xFFFF).max()}; first-seam waits max {(y[:, 6] >> 16).max()}")
+o_ = np.argsort(y[:, 7])
+print("  look-back done (us) by block:", " ".join(f"{v / f:.1f}" for v in y[o_, 3][:: max(1, len(y) // 16)]))
