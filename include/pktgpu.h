@@ -448,6 +448,16 @@ int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint
 int pkt_parse_pcap(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                    uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
 
+/* pkt_parse_pcap without the host wait, for a stream of captures: queues the index kernels and the
+ * counted parse on `stream` (cap <= 2^26) and returns.  Once the caller has synchronised `stream`,
+ * pkt_parse_pcap_result gives the outcome (the record count, or the errors of
+ * pkt_pcap_index_device; after an error nothing was parsed).  The ctx's index scratch belongs to
+ * the queued call until then: one capture in flight per ctx (two captures in flight = two ctxs,
+ * e.g. one per stream). */
+int pkt_parse_pcap_async(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
+                         uint64_t *offsets, uint32_t *lens, uint64_t cap, void *stream);
+int pkt_parse_pcap_result(pkt_ctx_t *ctx, uint64_t *n_out);
+
 /* Packet::ipv4_checksum on the host (same arithmetic as the device kernel). */
 uint16_t pkt_ipv4_checksum_host(const uint8_t *hdr, size_t len);
 

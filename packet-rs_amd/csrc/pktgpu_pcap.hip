@@ -1092,14 +1092,11 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     return pcap_finish(ctx, n_out);
 }
 
-int pkt_parse_pcap(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
-                   uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out, void* stream) {
-    if (!ctx || !out || !n_out || !cap || !offsets || !lens) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
-    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
-    *n_out = 0;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+// The index kernels and the counted parse, queued on `stream` (no host wait).
+static int parse_pcap_queue(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                            uint64_t* offsets, uint32_t* lens, uint64_t cap, void* stream) {
     const uint64_t* count_dev = nullptr;
-    int rc = pcap_launch(ctx, buf, len, offsets, lens, cap, s, &count_dev);
+    int rc = pcap_launch(ctx, buf, len, offsets, lens, cap, reinterpret_cast<hipStream_t>(stream), &count_dev);
     if (rc != PKT_SUCCESS) return rc;
     pkt_batch_t b;
     b.slab = buf;
@@ -1109,15 +1106,46 @@ int pkt_parse_pcap(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, 
     b.stride = 0;
     b.reserved = 0;
     b.n = cap;
+    // one parse launch over cap records whose blocks past the device-produced count exit
+    return pktgpu_parse_counted(ctx, &b, entry, out, stream, count_dev);
+}
+
+int pkt_parse_pcap_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                         uint64_t* offsets, uint32_t* lens, uint64_t cap, void* stream) {
+    if (!ctx || !out || !cap || !offsets || !lens) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    if (cap > (1ull << 26)) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_async: cap > 2^26 records");
+    return parse_pcap_queue(ctx, buf, len, entry, out, offsets, lens, cap, stream);
+}
+
+int pkt_parse_pcap_result(pkt_ctx_t* ctx, uint64_t* n_out) {
+    if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    *n_out = 0;
+    return pcap_finish(ctx, n_out);
+}
+
+int pkt_parse_pcap(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                   uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!ctx || !out || !n_out || !cap || !offsets || !lens) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    *n_out = 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    int rc;
     if (cap <= (1ull << 26)) {
-        // one parse launch over cap records whose blocks past the device-produced count exit: the
-        // host waits once, for the index and the parse together
-        rc = pktgpu_parse_counted(ctx, &b, entry, out, stream, count_dev);
-        if (rc != PKT_SUCCESS) return rc;
+        // the host waits once, for the index and the parse together
+        if ((rc = parse_pcap_queue(ctx, buf, len, entry, out, offsets, lens, cap, stream)) != PKT_SUCCESS) return rc;
         const hipError_t e = hipStreamSynchronize(s);
         if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap");
         return pcap_finish(ctx, n_out);
     }
+    if ((rc = pcap_launch(ctx, buf, len, offsets, lens, cap, s, nullptr)) != PKT_SUCCESS) return rc;
+    pkt_batch_t b;
+    b.slab = buf;
+    b.slab_len = len;
+    b.offsets = offsets;
+    b.lens = lens;
+    b.stride = 0;
+    b.reserved = 0;
     // batches over 2^26 records take several launches: the count first
     hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap");

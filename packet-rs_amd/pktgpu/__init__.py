@@ -225,6 +225,26 @@ class Parser:
                                            self._stream(stream)), "pkt_parse_pcap")
         return n.value, res, offsets, lens
 
+    def parse_pcap_async(self, buf, cap, out, offsets, lens, entry="parse", stream=None):
+        """pkt_parse_pcap_async: queue the index and the parse of the capture in `buf` on `stream`
+        (no host wait) into the caller's `out` / `offsets` / `lens` (sized for cap records).  Take
+        the outcome with pcap_result() after synchronising the stream; one capture in flight per
+        Parser."""
+        torch = _torch()
+        assert buf.dtype == torch.uint8 and buf.is_cuda and buf.is_contiguous()
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        o = out if isinstance(out, self._lib.PktOut) else self.out_struct(out)
+        self._check(self._L.pkt_parse_pcap_async(self._ctx, buf.data_ptr(), buf.numel(), e, ctypes.byref(o),
+                                                 offsets.data_ptr(), lens.data_ptr(), int(cap),
+                                                 self._stream(stream)), "pkt_parse_pcap_async")
+
+    def pcap_result(self):
+        """pkt_parse_pcap_result: the record count of the last parse_pcap_async (its stream
+        synchronised first by the caller); raises on its errors."""
+        n = ctypes.c_uint64()
+        self._check(self._L.pkt_parse_pcap_result(self._ctx, ctypes.byref(n)), "pkt_parse_pcap_result")
+        return n.value
+
     def parse_pcap_host(self, buf, cap, entry="parse", columns="all", out=None, index=True):
         """pkt_parse_pcap_host: a pcap file in host memory (numpy uint8 / bytes; pinned via host_empty
         for the full link rate) -> (n records, {column: numpy array} sized for `cap` records, slot

@@ -106,6 +106,9 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_uint64), _P]),
     "pkt_parse_pcap": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut), _P, _P,
                                       ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), _P]),
+    "pkt_parse_pcap_async": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut), _P, _P,
+                                            ctypes.c_uint64, _P]),
+    "pkt_parse_pcap_result": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_ipv4_checksum_host": (ctypes.c_uint16, [ctypes.c_char_p, ctypes.c_size_t]),
     # packed outputs + multi-GPU (pkt_mgpu_*)
     "pkt_out_packed": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, _P, ctypes.POINTER(PktOut),

@@ -168,6 +168,56 @@ def test_one_ctx_growing_and_shrinking_captures():
         P2.close()
 
 
+def test_parse_pcap_async_two_ctx(P):
+    """pkt_parse_pcap_async / pkt_parse_pcap_result: captures queued alternately on two ctxs and two
+    streams (one in flight per ctx), each result equal to the host indexer + oracle; an error
+    capture parses nothing and its result raises."""
+    import torch
+    import pktgpu
+    P2 = pktgpu.Parser(0)
+    try:
+        ps, ss = [P, P2], [torch.cuda.Stream(), torch.cuda.Stream()]
+        caps = [gen.gen_c4(n, seed=90 + n) for n in (30000, 4097, 65536, 1, 20000)]
+        bad = records([b"\x01" * 60, b"\x02" * 70, b"\x03" * 80])[:-3]
+        jobs = [(c[0], len(c[1]), c) for c in caps] + [(np.frombuffer(bad, np.uint8), 8, None)]
+        slots = [None, None]
+        def finish(j):
+            buf_d, res, o, l, c = slots[j]
+            ss[j].synchronize()
+            if c is None:
+                with pytest.raises(RuntimeError):
+                    ps[j].pcap_result()
+                assert (res["status"].cpu().numpy() == 0xEE).all()
+                return
+            assert ps[j].pcap_result() == len(c[1])
+            assert np.array_equal(o.cpu().numpy(), c[1]) and np.array_equal(l.cpu().numpy(), c[2])
+            ref = oracle.parse_batch(c[0], len(c[1]), offsets=c[1], lens=c[2], columns=list(res), nthreads=8)
+            for k, ov in ref.items():
+                gv = res[k].cpu().numpy()
+                if k in ("hdr_type", "hdr_off"):
+                    valid = np.arange(schema.MAX_HDRS)[:, None] < ref["n_hdrs"].astype(np.int64)[None, :]
+                    assert not (valid & (gv != ov)).any(), k
+                else:
+                    assert np.array_equal(gv, ov), k
+        for k, (buf, cap, c) in enumerate(jobs):
+            j = k % 2
+            if slots[j] is not None:
+                finish(j)
+            cols = ["status"] if c is None else ["chain", "ipv4", "udp", "tcp"]
+            res = ps[j].alloc(cap, cols)
+            res["status"].fill_(0xEE)
+            bd = dev(buf)
+            o = torch.empty(cap, dtype=torch.uint64, device="cuda")
+            l = torch.empty(cap, dtype=torch.uint32, device="cuda")
+            ss[j].wait_stream(torch.cuda.current_stream())
+            ps[j].parse_pcap_async(bd, cap, res, o, l, stream=ss[j])
+            slots[j] = (bd, res, o, l, c)
+        for j in (0, 1):
+            finish(j)
+    finally:
+        P2.close()
+
+
 def test_parse_pcap_fused_vs_oracle(P):
     """pkt_parse_pcap: device index + parse in one call, the parse taking the record count from the
     device (one host synchronisation).  Columns sized for cap > count: slot rows strided by cap and
