@@ -312,6 +312,15 @@ int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pk
  * parsed).  Blocking.  One host call at a time per ctx. */
 int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                         uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out);
+/* pkt_parse_pcap_host without the wait, for a stream of captures (cap <= 2^26, every column of `out`
+ * in pinned memory from pkt_host_alloc, no index output): queues the file's copy in, the index and
+ * the parse (whose kernel writes the columns over the link) on the ctx's own stream and returns;
+ * `buf` and `out` must stay untouched until pkt_parse_pcap_host_result, which waits for them and
+ * gives the outcome as pkt_parse_pcap_host's (*n_out = the record count).  One capture in flight
+ * per ctx: two ctxs keep one capture's copy in flowing while the other's columns flow out. */
+int pkt_parse_pcap_host_async(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
+                              uint64_t cap);
+int pkt_parse_pcap_host_result(pkt_ctx_t *ctx, uint64_t *n_out);
 /* Pinned (page-locked) host memory for pkt_parse_host buffers. */
 int pkt_host_alloc(pkt_ctx_t *ctx, uint64_t bytes, void **p);
 int pkt_host_free(pkt_ctx_t *ctx, void *p);

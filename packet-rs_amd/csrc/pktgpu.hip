@@ -1299,18 +1299,17 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     return staged_parse(ctx, b, entry, out, chunk, false);
 }
 
-int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
-                        uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out) {
-    if (!ctx || !buf || !out || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
-    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
-    *n_out = 0;
+}  // extern "C"
+
+// The host pipeline's streams and the capture's device buffers (file + index, grown on demand; +16:
+// the kernels' readable tail), after the ctx's earlier host-path work has finished.
+static int pcap_host_buffers(pkt_ctx_t* ctx, uint64_t len, uint64_t cap) {
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     int rc = host_pipe_init(ctx);
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
     for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
-    // the file and its index on the device (grown on demand; +16: the kernels' readable tail)
     const uint64_t fbytes = ((len + 15) & ~(uint64_t)15) + 16;
     if (fbytes > hp.file_cap) {
         (void)hipFree(hp.file);
@@ -1332,6 +1331,56 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
         if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
         hp.idx_cap = c2;
     }
+    return PKT_SUCCESS;
+}
+
+extern "C" {
+
+int pkt_parse_pcap_host_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                              uint64_t cap) {
+    if (!ctx || !buf || !out || !cap) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    if (cap > kLaunchChunk) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host_async: cap > 2^26 records");
+    pkt_out_t dout;
+    if (!out_mapped(out, dout))
+        return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host_async: the columns must be pinned (pkt_host_alloc)");
+    int rc = pcap_host_buffers(ctx, len, cap);
+    if (rc != PKT_SUCCESS) return rc;
+    HostPipe& hp = ctx->hp;
+    hipStream_t s = hp.s[0];
+    hipError_t e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)");
+    const uint64_t* count_dev = nullptr;
+    if ((rc = pktgpu_pcap_launch(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, s, &count_dev)) != PKT_SUCCESS) return rc;
+    pkt_batch_t db;
+    db.slab = hp.file;
+    db.slab_len = len;
+    db.offsets = hp.ioffs;
+    db.lens = hp.ilens;
+    db.stride = 0;
+    db.reserved = 0;
+    db.n = cap;  // blocks past the device-produced count exit
+    return parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap, nullptr, count_dev);
+}
+
+int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
+    if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    *n_out = 0;
+    if (!ctx->hp.init) return fail(ctx, PKT_ERR_INVALID_ARG, "no capture queued on this ctx");
+    const hipError_t e = hipStreamSynchronize(ctx->hp.s[0]);
+    if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap_host_result");
+    return pktgpu_pcap_finish(ctx, n_out);
+}
+
+int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                        uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out) {
+    if (!ctx || !buf || !out || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
+    *n_out = 0;
+    hipError_t e;
+    int rc = pcap_host_buffers(ctx, len, cap);
+    if (rc != PKT_SUCCESS) return rc;
+    HostPipe& hp = ctx->hp;
     hipStream_t s = hp.s[0];
     // in: the whole file, one copy (the record chain is sequential: the index needs all of it)
     if ((e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s)) != hipSuccess)

@@ -103,3 +103,10 @@ int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, con
 // count_dev is given.  Used by pkt_parse_pcap (pktgpu_pcap.hip).
 int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, void* stream,
                          const uint64_t* count_dev, uint64_t slot_stride = 0);
+
+// The device pcap indexer's kernels queued on `stream` (no host wait; *count_dev = the device word
+// holding the record count, 0 after an error), and its outcome once the stream has passed them
+// (pktgpu_pcap.hip).  Used by pkt_parse_pcap_host_async (pktgpu.hip).
+int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev);
+int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out);

@@ -1064,11 +1064,18 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
 // The outcome of the last pcap_launch (the stream has been synchronised).
 static int pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) {
     const PcapScratch& pc = ctx->pc;
+    if (!pc.ctl) return fail(ctx, PKT_ERR_INVALID_ARG, "no capture was indexed on this ctx");
     if (!pc.ctl[kHostMagic]) return fail(ctx, PKT_ERR_INVALID_ARG, "bad pcap magic");
     if (pc.ctl[kHostErr]) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap record runs past the end of the buffer");
     *n_out = pc.ctl[kHostTotal];
     return PKT_SUCCESS;
 }
+
+int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev) {
+    return pcap_launch(ctx, buf, len, offsets, lens, cap, s, count_dev);
+}
+int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) { return pcap_finish(ctx, n_out); }
 
 extern "C" {
 

@@ -245,6 +245,23 @@ class Parser:
         self._check(self._L.pkt_parse_pcap_result(self._ctx, ctypes.byref(n)), "pkt_parse_pcap_result")
         return n.value
 
+    def parse_pcap_host_async(self, buf, cap, out, entry="parse"):
+        """pkt_parse_pcap_host_async: queue copy-in, index and parse of the capture in pinned host
+        memory `buf` (numpy uint8 from host_empty) into the pinned columns `out` ({column: numpy
+        array from host_empty}, sized for cap records); pcap_host_result() waits and returns the
+        record count.  One capture in flight per Parser."""
+        e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
+        o = self._lib.PktOut()
+        for c, v in out.items():
+            setattr(o, c, v.ctypes.data if v.size else None)
+        self._check(self._L.pkt_parse_pcap_host_async(self._ctx, buf.ctypes.data, buf.size, e, ctypes.byref(o),
+                                                      int(cap)), "pkt_parse_pcap_host_async")
+
+    def pcap_host_result(self):
+        n = ctypes.c_uint64()
+        self._check(self._L.pkt_parse_pcap_host_result(self._ctx, ctypes.byref(n)), "pkt_parse_pcap_host_result")
+        return n.value
+
     def parse_pcap_host(self, buf, cap, entry="parse", columns="all", out=None, index=True):
         """pkt_parse_pcap_host: a pcap file in host memory (numpy uint8 / bytes; pinned via host_empty
         for the full link rate) -> (n records, {column: numpy array} sized for `cap` records, slot

@@ -106,6 +106,9 @@ SIGNATURES = {
                                              ctypes.POINTER(ctypes.c_uint64), _P]),
     "pkt_parse_pcap": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut), _P, _P,
                                       ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), _P]),
+    "pkt_parse_pcap_host_async": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut),
+                                                 ctypes.c_uint64]),
+    "pkt_parse_pcap_host_result": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_parse_pcap_async": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut), _P, _P,
                                             ctypes.c_uint64, _P]),
     "pkt_parse_pcap_result": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

@@ -172,3 +172,50 @@ def test_pcap_host_cap_and_errors(P):
             P.parse_pcap_host(bad, 64)
     m, g, _ = P.parse_pcap_host(pc, 22, columns=["chain"])
     assert m == 22 and int(g["status"].max()) == 0
+
+
+def test_pcap_host_async_two_ctx(P):
+    """pkt_parse_pcap_host_async / _result: captures in pinned host memory queued alternately on two
+    ctxs (one in flight per ctx, one capture's copy in overlapping the other's columns out), every
+    result equal to the oracle; an error capture parses nothing and its result raises; pageable
+    columns are refused."""
+    import pktgpu
+    P2 = pktgpu.Parser(0)
+    try:
+        ps = [P, P2]
+        caps = [gen.gen_c4(n, seed=60 + n) for n in (20000, 1, 65536, 4097)]
+        pc = open(os.path.join(GOLD, "ref22.pcap"), "rb").read()
+        jobs = [(c[0], len(c[1]), c) for c in caps] + [(np.frombuffer(pc[:-3], np.uint8), 64, None)]
+        slots = [None, None]
+
+        def finish(j):
+            res, hb, c = slots[j]
+            if c is None:
+                with pytest.raises(RuntimeError):
+                    ps[j].pcap_host_result()
+                assert (res["status"] == 0xEE).all()  # an error parses nothing
+                return
+            n = len(c[1])
+            assert ps[j].pcap_host_result() == n
+            ref = oracle.parse_batch(c[0], n, offsets=c[1], lens=c[2], columns=list(res), nthreads=8)
+            check(res, ref, f"async host capture n={n}")
+
+        for k, (buf, cap, c) in enumerate(jobs):
+            j = k % 2
+            if slots[j] is not None:
+                finish(j)
+            hb = ps[j].host_empty((buf.size,), np.uint8)
+            hb[:] = buf
+            cols = ["status"] if c is None else list(schema.COLUMN_NAMES)
+            res = {col: ps[j].host_empty(schema.column_shape(col, cap), schema.column_dtype(col)) for col in cols}
+            res["status"][:] = 0xEE
+            ps[j].parse_pcap_host_async(hb, cap, res)
+            slots[j] = (res, hb, c)
+        for j in (0, 1):
+            finish(j)
+        buf, offs, lens = caps[0]
+        with pytest.raises(RuntimeError):  # pageable columns: refused
+            P.parse_pcap_host_async(P.host_empty((buf.size,), np.uint8), len(offs),
+                                    {"status": np.zeros(len(offs), np.uint8)})
+    finally:
+        P2.close()
