@@ -317,7 +317,8 @@ int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int en
  * the parse (whose kernel writes the columns over the link) on the ctx's own stream and returns;
  * `buf` and `out` must stay untouched until pkt_parse_pcap_host_result, which waits for them and
  * gives the outcome as pkt_parse_pcap_host's (*n_out = the record count).  One capture in flight
- * per ctx: two ctxs keep one capture's copy in flowing while the other's columns flow out. */
+ * per ctx (as pkt_parse_pcap_async): two ctxs keep one capture's copy in flowing while the other's
+ * columns flow out. */
 int pkt_parse_pcap_host_async(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                               uint64_t cap);
 int pkt_parse_pcap_host_result(pkt_ctx_t *ctx, uint64_t *n_out);
@@ -458,11 +459,11 @@ int pkt_parse_pcap(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, 
                    uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
 
 /* pkt_parse_pcap without the host wait, for a stream of captures: queues the index kernels and the
- * counted parse on `stream` (cap <= 2^26) and returns.  Once the caller has synchronised `stream`,
- * pkt_parse_pcap_result gives the outcome (the record count, or the errors of
- * pkt_pcap_index_device; after an error nothing was parsed).  The ctx's index scratch belongs to
- * the queued call until then: one capture in flight per ctx (two captures in flight = two ctxs,
- * e.g. one per stream). */
+ * counted parse on `stream` (cap <= 2^26) and returns.  pkt_parse_pcap_result waits for them and
+ * gives the outcome (the record count, or the errors of pkt_pcap_index_device; after an error
+ * nothing was parsed).  The ctx's index scratch belongs to the queued capture until its result is
+ * taken: one capture in flight per ctx (two in flight = two ctxs, e.g. one per stream); another
+ * index call on the ctx before that fails with PKT_ERR_INVALID_ARG. */
 int pkt_parse_pcap_async(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                          uint64_t *offsets, uint32_t *lens, uint64_t cap, void *stream);
 int pkt_parse_pcap_result(pkt_ctx_t *ctx, uint64_t *n_out);

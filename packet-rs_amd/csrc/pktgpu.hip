@@ -1304,6 +1304,8 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
 // The host pipeline's streams and the capture's device buffers (file + index, grown on demand; +16:
 // the kernels' readable tail), after the ctx's earlier host-path work has finished.
 static int pcap_host_buffers(pkt_ctx_t* ctx, uint64_t len, uint64_t cap) {
+    if (ctx->pc.pending)
+        return fail(ctx, PKT_ERR_INVALID_ARG, "a queued capture's outcome has not been taken on this ctx (pkt_parse_pcap_result)");
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
     int rc = host_pipe_init(ctx);
@@ -1360,16 +1362,19 @@ int pkt_parse_pcap_host_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, 
     db.stride = 0;
     db.reserved = 0;
     db.n = cap;  // blocks past the device-produced count exit
-    return parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap, nullptr, count_dev);
+    if ((rc = parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap, nullptr, count_dev)) != PKT_SUCCESS) {
+        (void)hipStreamSynchronize(s);  // nothing left in flight
+        return rc;
+    }
+    ctx->pc.pending = true;
+    ctx->pc.pending_stream = s;
+    return PKT_SUCCESS;
 }
 
 int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
     if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     *n_out = 0;
-    if (!ctx->hp.init) return fail(ctx, PKT_ERR_INVALID_ARG, "no capture queued on this ctx");
-    const hipError_t e = hipStreamSynchronize(ctx->hp.s[0]);
-    if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap_host_result");
-    return pktgpu_pcap_finish(ctx, n_out);
+    return pktgpu_pcap_take(ctx, n_out);
 }
 
 int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,

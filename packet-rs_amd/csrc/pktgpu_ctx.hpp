@@ -36,6 +36,10 @@ struct PcapScratch {
     uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the kernel writes them)
     uint32_t epoch = 0;           // per call: block states of older calls are ignored, not cleared
     uint32_t scan_resident = 0;   // scan-kernel blocks resident at once (0 = not yet queried)
+    // a capture queued by pkt_parse_pcap_async / pkt_parse_pcap_host_async whose outcome (the words
+    // above) has not been taken yet: no other index call may reuse the scratch until it is
+    bool pending = false;
+    hipStream_t pending_stream = nullptr;
 };
 
 // Element size of each pkt_out_t column, in declaration order (slot columns: one slot; the
@@ -110,3 +114,4 @@ int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const 
 int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                        uint64_t cap, hipStream_t s, const uint64_t** count_dev);
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out);
+int pktgpu_pcap_take(pkt_ctx_t* ctx, uint64_t* n_out);  // a queued capture's outcome (waits; clears pending)

@@ -983,6 +983,8 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     if (!ctx || !buf || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
+    if (ctx->pc.pending)
+        return fail(ctx, PKT_ERR_INVALID_ARG, "a queued capture's outcome has not been taken on this ctx (pkt_parse_pcap_result)");
     const uint64_t K64 = (len + kRegion - 1) / kRegion;
     if (K64 > (1ull << 31) || len >= kValMask) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
     const uint32_t K = (uint32_t)K64, nb = (K + kScanRegions - 1) / kScanRegions;
@@ -1077,6 +1079,17 @@ int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
 }
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) { return pcap_finish(ctx, n_out); }
 
+// The outcome of the capture queued on ctx (waits for it).
+int pktgpu_pcap_take(pkt_ctx_t* ctx, uint64_t* n_out) {
+    PcapScratch& pc = ctx->pc;
+    if (!pc.pending) return fail(ctx, PKT_ERR_INVALID_ARG, "no capture queued on this ctx");
+    const hipError_t e = hipStreamSynchronize(pc.pending_stream);
+    pc.pending = false;
+    pc.pending_stream = nullptr;
+    if (e != hipSuccess) return hip_fail(ctx, e, "pkt_parse_pcap_result");
+    return pcap_finish(ctx, n_out);
+}
+
 extern "C" {
 
 #if PKTGPU_STAMPS
@@ -1122,13 +1135,20 @@ int pkt_parse_pcap_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int e
     if (!ctx || !out || !cap || !offsets || !lens) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (cap > (1ull << 26)) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_async: cap > 2^26 records");
-    return parse_pcap_queue(ctx, buf, len, entry, out, offsets, lens, cap, stream);
+    const int rc = parse_pcap_queue(ctx, buf, len, entry, out, offsets, lens, cap, stream);
+    if (rc != PKT_SUCCESS) {
+        (void)hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream));  // nothing left in flight
+        return rc;
+    }
+    ctx->pc.pending = true;
+    ctx->pc.pending_stream = reinterpret_cast<hipStream_t>(stream);
+    return PKT_SUCCESS;
 }
 
 int pkt_parse_pcap_result(pkt_ctx_t* ctx, uint64_t* n_out) {
     if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     *n_out = 0;
-    return pcap_finish(ctx, n_out);
+    return pktgpu_pcap_take(ctx, n_out);
 }
 
 int pkt_parse_pcap(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,

@@ -227,9 +227,8 @@ class Parser:
 
     def parse_pcap_async(self, buf, cap, out, offsets, lens, entry="parse", stream=None):
         """pkt_parse_pcap_async: queue the index and the parse of the capture in `buf` on `stream`
-        (no host wait) into the caller's `out` / `offsets` / `lens` (sized for cap records).  Take
-        the outcome with pcap_result() after synchronising the stream; one capture in flight per
-        Parser."""
+        (no host wait) into the caller's `out` / `offsets` / `lens` (sized for cap records).
+        pcap_result() waits for it and returns the record count; one capture in flight per Parser."""
         torch = _torch()
         assert buf.dtype == torch.uint8 and buf.is_cuda and buf.is_contiguous()
         e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
@@ -239,8 +238,8 @@ class Parser:
                                                  self._stream(stream)), "pkt_parse_pcap_async")
 
     def pcap_result(self):
-        """pkt_parse_pcap_result: the record count of the last parse_pcap_async (its stream
-        synchronised first by the caller); raises on its errors."""
+        """pkt_parse_pcap_result: waits for the queued parse_pcap_async and returns its record
+        count; raises on its errors."""
         n = ctypes.c_uint64()
         self._check(self._L.pkt_parse_pcap_result(self._ctx, ctypes.byref(n)), "pkt_parse_pcap_result")
         return n.value

@@ -214,6 +214,20 @@ def test_parse_pcap_async_two_ctx(P):
             slots[j] = (bd, res, o, l, c)
         for j in (0, 1):
             finish(j)
+        # the scratch belongs to a queued capture until its result is taken
+        buf, offs, lens = caps[0]
+        bd, m = dev(buf), len(offs)
+        res = P.alloc(m, ["status"])
+        o = torch.empty(m, dtype=torch.uint64, device="cuda")
+        l = torch.empty(m, dtype=torch.uint32, device="cuda")
+        P.parse_pcap_async(bd, m, res, o, l)
+        with pytest.raises(RuntimeError):
+            P.parse_pcap_async(bd, m, res, o, l)
+        with pytest.raises(RuntimeError):
+            P.parse_pcap(bd, m)
+        assert P.pcap_result() == m
+        with pytest.raises(RuntimeError):
+            P.pcap_result()
     finally:
         P2.close()
 
