@@ -850,6 +850,11 @@ int pkt_ctx_create(int device, pkt_ctx_t** out) {
 }
 
 int pkt_ctx_destroy(pkt_ctx_t* ctx) {
+    if (ctx && ctx->tv_flag) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ctx->tv_flag);
+    }
     if (ctx && ctx->mx.dev) {
         (void)hipSetDevice(ctx->device);
         (void)hipDeviceSynchronize();

@@ -82,6 +82,7 @@ struct pkt_ctx {
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
+    uint32_t* tv_flag = nullptr;  // pkt_to_vec_batch: a device word, nonzero = the records overlap a chunk
     std::string err;
 };
 

@@ -275,7 +275,44 @@ struct TParams {
     uint64_t dst_len;
     const uint64_t* dst_offsets;
     uint32_t* out_len;
+    const uint32_t* overlap;  // PKTGPU_TOVEC_RMW: device word, 0 = no 16-byte chunk holds bytes of two records
 };
+
+// Edge chunks by read-modify-write (PKTGPU_TOVEC_RMW): in the input's own layout of an indexed
+// batch whose records are in order with no 16-byte chunk shared by two of them (a capture: the
+// 16-byte record headers lie between them), a packet's partial head / tail chunk is read from the
+// destination, its bytes merged in, and the chunk stored whole — one load and one 16-byte store
+// instead of up to eight dword / short / byte stores run by the whole wave for any lane's edge, and
+// the destination's bytes outside the packets are rewritten with their own values (no other lane
+// or wave touches that chunk).  tv_overlap_kernel decides per batch.
+#ifndef PKTGPU_TOVEC_RMW
+#define PKTGPU_TOVEC_RMW 1
+#endif
+__global__ __launch_bounds__(256) void tv_overlap_kernel(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
+                                                         uint64_t n, uint32_t* flag) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x + 1;  // pairs (i - 1, i)
+    bool bad = false;
+    if (i < n) {
+        const uint64_t o0 = offs[i - 1], l0 = lens[i - 1], o1 = offs[i];
+        bad = l0 == 0 || ((o0 + l0 - 1) >> 4) >= (o1 >> 4);
+    }
+    if (__ballot(bad) && (threadIdx.x & 63u) == 0) atomicOr(flag, 1u);
+}
+
+// bytes [lo, hi) of the 16-byte chunk at ca from o, the rest from d (the destination's own bytes)
+__device__ __forceinline__ void merge_chunk(uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4],
+                                            uint32_t (&d)[4]) {
+    const uint32_t a = (uint32_t)(lo - ca), z = (uint32_t)(hi - ca);  // 0 <= a < z <= 16
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        // byte b of dword j is in [a, z) iff a <= 4j + b < z
+        const int32_t s0 = (int32_t)a - 4 * j, s1 = (int32_t)z - 4 * j;
+        const uint32_t m0 = s0 <= 0 ? ~0u : (s0 >= 4 ? 0u : ~0u << (8 * s0));
+        const uint32_t m1 = s1 >= 4 ? ~0u : (s1 <= 0 ? 0u : ~0u >> (8 * (4 - s1)));
+        const uint32_t m = m0 & m1;
+        d[j] = (o[j] & m) | (d[j] & ~m);
+    }
+}
 
 __device__ __forceinline__ void put_byte(const TParams& p, uint64_t q, uint32_t v) {
     if (q < p.dst_len) p.dst[q] = (uint8_t)v;
@@ -477,7 +514,9 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     // 4 or 8 rounds' loads ahead was slower: C2 45 / 141 vs 33 us, C4 135 / 422 vs 125 us — 120+
     // VGPRs halve the resident waves, profiles/ab/r02tv_to_vec_unroll.txt.)
     uint32_t k = 0;
-    auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4]) {
+    // uniform: edge chunks by read-modify-write (the batch's records never share a chunk)
+    const bool rmw = PKTGPU_TOVEC_RMW && p.overlap && __builtin_amdgcn_readfirstlane(*p.overlap) == 0;
+    auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4], uint32_t (&dd)[4]) {
         uint64_t s, d;
         uint32_t L, pre;
         if (use_map) {  // rounds are located in order, each once
@@ -494,9 +533,18 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
         load_src_chunk(p.b, last16, s, d, ca, o);
         lo = ca > d ? ca : d;
         hi = ca + 16 < d + L ? ca + 16 : d + L;
+        if (rmw && !(lo == ca && hi == ca + 16) && ca + 16 <= p.dst_len) {  // the edge's own destination bytes
+            const uint4 v = *reinterpret_cast<const uint4*>(p.dst + ca);
+            dd[0] = v.x, dd[1] = v.y, dd[2] = v.z, dd[3] = v.w;
+        }
     };
-    auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4]) {
-        if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
+    auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4], uint32_t (&dd)[4]) {
+        if (rmw && !(lo == ca && hi == ca + 16) && ca + 16 <= p.dst_len) {
+            // (storing whole chunks through this same merged store too, one store per round: C4
+            // 143 vs 136 us, packed and C2 slower as well: profiles/ab/r04z_to_vec_rmw_edges.txt)
+            merge_chunk(ca, lo, hi, o, dd);
+            *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(dd[0], dd[1], dd[2], dd[3]);
+        } else if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
             if (dense) {
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 __builtin_nontemporal_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(p.dst + ca));
@@ -510,22 +558,23 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     if (total <= 4u * 64u) {  // short waves (C2: 4 rounds): the plain loop is faster (33.7 vs 34.4 us)
         for (uint32_t g = lane; g < total; g += 64u) {
             uint64_t ca, lo, hi;
-            uint32_t o[4];
-            locate(g, ca, lo, hi, o);
-            put(ca, lo, hi, o);
+            uint32_t o[4], dd[4] = {0, 0, 0, 0};
+            locate(g, ca, lo, hi, o, dd);
+            put(ca, lo, hi, o, dd);
         }
     } else {  // C4: 142 vs 148 us in the input's layout, 124 vs 138 us packed (two rounds ahead:
               // 141 / 108 vs 142 / 105 us, round 3, profiles/ab/r03g_to_vec_lookahead2.txt)
         uint64_t ca = 0, lo = 0, hi = 0;
-        uint32_t o[4] = {0, 0, 0, 0};
-        locate(lane, ca, lo, hi, o);  // lane < 256 < total
+        uint32_t o[4] = {0, 0, 0, 0}, dd[4] = {0, 0, 0, 0};
+        locate(lane, ca, lo, hi, o, dd);  // lane < 256 < total
         for (uint32_t g = lane; g < total; g += 64u) {
             uint64_t ca1 = 0, lo1 = 0, hi1 = 0;
-            uint32_t o1[4] = {0, 0, 0, 0};
-            if (g + 64u < total) locate(g + 64u, ca1, lo1, hi1, o1);
-            put(ca, lo, hi, o);
+            uint32_t o1[4] = {0, 0, 0, 0}, dd1[4] = {0, 0, 0, 0};
+            if (g + 64u < total) locate(g + 64u, ca1, lo1, hi1, o1, dd1);
+            put(ca, lo, hi, o, dd);
             ca = ca1, lo = lo1, hi = hi1;
             o[0] = o1[0], o[1] = o1[1], o[2] = o1[2], o[3] = o1[3];
+            dd[0] = dd1[0], dd[1] = dd1[1], dd[2] = dd1[2], dd[3] = dd1[3];
         }
     }
     // ---- Q2 packets (two or more GRE options), one at a time by the whole wave: output byte q
@@ -919,6 +968,18 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
     tp.dst_len = dst_len;
     tp.dst_offsets = dst_offsets;
     tp.out_len = out_len;
+    tp.overlap = nullptr;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (PKTGPU_TOVEC_RMW && !dst_offsets && b->offsets && b->lens && b->n > 1) {
+        // does any 16-byte chunk hold bytes of two records?  (one pass over the index: 12 B/record)
+        if (!ctx->tv_flag && (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), 256)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMalloc (to_vec flag)");
+        if ((e = hipMemsetAsync(ctx->tv_flag, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
+        hipLaunchKernelGGL(tv_overlap_kernel, dim3((unsigned)((b->n - 1 + 255) / 256)), dim3(256), 0, s, b->offsets,
+                           b->lens, b->n, ctx->tv_flag);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "tv_overlap_kernel launch");
+        tp.overlap = ctx->tv_flag;
+    }
     hipLaunchKernelGGL(to_vec_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), tp);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
     return PKT_SUCCESS;

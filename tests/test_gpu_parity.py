@@ -447,6 +447,40 @@ def test_to_vec_c4_dst_layouts_vs_oracle(P, shift):
     assert (o[mask] == 0xEE).all()
 
 
+@pytest.mark.parametrize("gap", [16, 5])
+def test_to_vec_input_layout_edges_vs_oracle(P, gap):
+    """to_vec into the input's own layout (dst_offsets NULL) of an indexed batch: with 16-byte gaps
+    between the records (a capture's record headers) no 16-byte chunk holds two records' bytes and
+    the partial edge chunks are read-modify-written whole; with 5-byte gaps neighbouring records share
+    chunks and the kernel keeps the byte-exact edge stores.  Every to_vec equals the oracle and no
+    byte outside the written packets changes."""
+    n = 20000
+    slab0, offs0, lens = gen.gen_c4(n, seed=77 + gap)
+    rng = np.random.default_rng(gap)
+    cut = rng.random(n) < 0.02  # truncated records: nothing written
+    lens = np.where(cut, np.maximum(1, (lens * rng.random(n)).astype(np.uint32)), lens).astype(np.uint32)
+    offs = np.concatenate([[24 + gap], 24 + gap + np.cumsum(lens.astype(np.uint64) + np.uint64(gap))[:-1]]).astype(np.uint64)
+    total = int(offs[-1]) + int(lens[-1]) + 32
+    buf = np.zeros(total, np.uint8)
+    for i in range(n):
+        a, b = int(offs0[i]), int(offs[i])
+        buf[b:b + int(lens[i])] = slab0[a:a + int(lens[i])]
+    ds, do, dl = dev(buf), dev(offs), dev(lens)
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst = torch.full((total,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst)
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    want, wl = oracle.round_trip_batch(buf, n, offsets=offs, lens=lens, slow=True, nthreads=8)
+    assert np.array_equal(ln, wl)
+    mask = np.ones(total, bool)
+    for i in range(n):
+        a, k = int(offs[i]), int(wl[i])
+        assert o[a:a + k].tobytes() == want[a:a + k].tobytes(), i
+        mask[a:a + k] = False
+    assert (o[mask] == 0xEE).all()
+
+
 def test_to_vec_long_packets_both_chunk_maps_vs_oracle(P):
     """Waves whose outputs exceed the kernel's per-wave start map (> 2048 16-byte chunks: 64
     records of ~1.4 KB) next to waves of short records (the map path), in a pcap-like layout with
