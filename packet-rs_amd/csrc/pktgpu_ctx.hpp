@@ -82,7 +82,11 @@ struct pkt_ctx {
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
-    uint32_t* tv_flag = nullptr;  // pkt_to_vec_batch: a device word, nonzero = the records overlap a chunk
+    // pkt_to_vec_batch: device words, nonzero = a chunk holds bytes of two records; a ring, one word
+    // per call, so calls in flight on several streams never share one
+    static constexpr uint32_t kTvFlags = 256;
+    uint32_t* tv_flag = nullptr;
+    uint32_t tv_next = 0;
     std::string err;
 };
 

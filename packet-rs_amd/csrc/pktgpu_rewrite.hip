@@ -972,13 +972,15 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (PKTGPU_TOVEC_RMW && !dst_offsets && b->offsets && b->lens && b->n > 1) {
         // does any 16-byte chunk hold bytes of two records?  (one pass over the index: 12 B/record)
-        if (!ctx->tv_flag && (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), 256)) != hipSuccess)
+        if (!ctx->tv_flag &&
+            (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), pkt_ctx::kTvFlags * sizeof(uint32_t))) != hipSuccess)
             return hip_fail(ctx, e, "hipMalloc (to_vec flag)");
-        if ((e = hipMemsetAsync(ctx->tv_flag, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
+        uint32_t* flag = ctx->tv_flag + (ctx->tv_next++ % pkt_ctx::kTvFlags);
+        if ((e = hipMemsetAsync(flag, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
         hipLaunchKernelGGL(tv_overlap_kernel, dim3((unsigned)((b->n - 1 + 255) / 256)), dim3(256), 0, s, b->offsets,
-                           b->lens, b->n, ctx->tv_flag);
+                           b->lens, b->n, flag);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "tv_overlap_kernel launch");
-        tp.overlap = ctx->tv_flag;
+        tp.overlap = flag;
     }
     hipLaunchKernelGGL(to_vec_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), tp);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
