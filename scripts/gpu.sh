@@ -17,6 +17,7 @@
 #   stamps             per-wave segment stamps (needs lib/variants/stamps.so: build_variant.sh stamps -DPKTGPU_STAMPS=1)
 #   pcapab             pcap indexer variants lib/variants/*.so, interleaved (scripts/pcap_index_bench.py)
 #   pcap               pcap indexer rate + rocprofv3 kernel stats of it
+#   pcapstamps         guess-wave / scan-block segment stamps (lib/variants/stamps.so, scripts/pcap_stamps.py)
 #   secondary          §8(f) kernels: scripts/secondary_bench.py + rocprofv3 kernel stats
 #   host               host-memory path rates (scripts/hostpath_native.py, pinned and pageable)
 #   ab=CFGS:VARS       every lib/variants/*.so through kbench, interleaved (scripts/ab.sh)
