@@ -571,10 +571,47 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
 
 // Block-wide exclusive composition of the threads' aggregates in thread order (all 256 threads).
 // Also returns `idx`: the thread index of the nearest claiming (non-none) aggregate before t, or -1.
+// The wave's inclusive scan by DPP moves (PKTGPU_PCAP_DPP): row_shr 1, 2, 4, 8 within each row of
+// 16 lanes, then row_bcast 15 and 31 across rows — register moves, no LDS; a lane without a source
+// takes the identity (update_dpp's `old`, bound_ctrl off), so every lane combines, without
+// divergence.  (The __shfl_up form below — ds_bpermute round trips, each step under `lane >= d` —
+// made the first block composition 2.8 us of every scan block, profiles/pcap/r04h2_stamps.txt.)
+#ifndef PKTGPU_PCAP_DPP
+#define PKTGPU_PCAP_DPP 1
+#endif
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
+    return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(old >> 32), (uint32_t)(v >> 32)) << 32) |
+           dpp32<CTRL, ROWS>((uint32_t)old, (uint32_t)v);
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ void scan_step(Agg& x, int32_t& ix) {
+    Agg y;
+    y.first = dpp64<CTRL, ROWS>(0, x.first);
+    y.last = dpp64<CTRL, ROWS>(0, x.last);
+    y.cnt = dpp64<CTRL, ROWS>(0, x.cnt);
+    y.bits = dpp32<CTRL, ROWS>(kBitNone, x.bits);
+    const int32_t iy = (int32_t)dpp32<CTRL, ROWS>(0xFFFFFFFFu, (uint32_t)ix);
+    x = combine(y, x);
+    ix = ix >= 0 ? ix : iy;
+}
+
 __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, int32_t* widx, Agg& total) {
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     int32_t ix = (a.bits & kBitNone) ? -1 : (int32_t)t;
     Agg x = a;
+    if constexpr (PKTGPU_PCAP_DPP) {
+        scan_step<0x111, 0xF>(x, ix);  // row_shr:1
+        scan_step<0x112, 0xF>(x, ix);  // row_shr:2
+        scan_step<0x114, 0xF>(x, ix);  // row_shr:4
+        scan_step<0x118, 0xF>(x, ix);  // row_shr:8
+        scan_step<0x142, 0xA>(x, ix);  // row_bcast:15 into rows 1 and 3
+        scan_step<0x143, 0xC>(x, ix);  // row_bcast:31 into rows 2 and 3
+    } else {
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan within the wave
         Agg y;
@@ -587,6 +624,7 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
             x = combine(y, x);
             ix = ix >= 0 ? ix : iy;
         }
+    }
     }
     if (lane == 63) {
         wtot[w] = x;
@@ -603,14 +641,23 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
     for (uint32_t q = 0; q < (uint32_t)kWaves; q++) total = combine(total, wtot[q]);
     // exclusive: the wave prefix before this lane
     Agg ex;
-    ex.first = __shfl_up(x.first, 1, 64);
-    ex.last = __shfl_up(x.last, 1, 64);
-    ex.cnt = __shfl_up(x.cnt, 1, 64);
-    ex.bits = __shfl_up(x.bits, 1, 64);
-    int32_t iex = __shfl_up(ix, 1, 64);
-    if (lane == 0) {
-        ex = agg_identity();
-        iex = -1;
+    int32_t iex;
+    if constexpr (PKTGPU_PCAP_DPP) {  // wave_shr:1, lane 0 the identity
+        ex.first = dpp64<0x138, 0xF>(0, x.first);
+        ex.last = dpp64<0x138, 0xF>(0, x.last);
+        ex.cnt = dpp64<0x138, 0xF>(0, x.cnt);
+        ex.bits = dpp32<0x138, 0xF>(kBitNone, x.bits);
+        iex = (int32_t)dpp32<0x138, 0xF>(0xFFFFFFFFu, (uint32_t)ix);
+    } else {
+        ex.first = __shfl_up(x.first, 1, 64);
+        ex.last = __shfl_up(x.last, 1, 64);
+        ex.cnt = __shfl_up(x.cnt, 1, 64);
+        ex.bits = __shfl_up(x.bits, 1, 64);
+        iex = __shfl_up(ix, 1, 64);
+        if (lane == 0) {
+            ex = agg_identity();
+            iex = -1;
+        }
     }
     idx = iex >= 0 ? iex : ib;
     __syncthreads();  // wtot / widx reusable
@@ -647,6 +694,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
 #if PKTGPU_STAMPS
     uint64_t st_[5] = {0, 0, 0, 0, 0};
     uint32_t n_fix = 0, n_wait = 0;
+    uint64_t t_bx = 0;  // after the first block composition
 #endif
     PCAP_STAMP(0);
     // the block order: blockIdx when every block of the grid is resident at once (the host checks
@@ -725,6 +773,13 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
         int32_t j;
         const Agg pre = block_exclusive(mine, j, wtot, widx, total);
+#if PKTGPU_STAMPS
+        if (!t_bx) {
+            __builtin_amdgcn_sched_barrier(0);
+            asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_bx)::"memory");
+            __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
         pre_cur = pre;
         const bool bad = j >= 0 && seam_bad(pre, mine);
         sbad[t] = bad;
@@ -929,7 +984,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         for (int q = 0; q < 5; q++) d[q] = st_[q];
         d[5] = n_fix;
         d[6] = n_wait;
-        d[7] = blk;
+        d[7] = t_bx;
     }
 #endif
 }
@@ -940,9 +995,15 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
                                                         uint64_t* __restrict__ offsets,
                                                         uint32_t* __restrict__ lens) {
     __shared__ uint32_t cpre[kEmitRegions + 1];
+    __shared__ uint64_t cex[kEmitRegions];
     const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
+    // every per-block value in one round trip: the block's first record index, the 16 regions'
+    // counts and exits (the exit ends each region's last record)
+    const uint64_t first = S.rpre[k0];
     if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
-        const uint32_t c = t < kEmitRegions && k0 + t < K ? (S.rcnt[k0 + t] & kCntMask) : 0;
+        const bool in = t < kEmitRegions && k0 + t < K;
+        const uint32_t c = in ? (S.rcnt[k0 + t] & kCntMask) : 0;
+        if (t < kEmitRegions) cex[t] = in ? S.rexit[k0 + t] : 0;
         uint32_t x = c;
 #pragma unroll
         for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
@@ -953,7 +1014,6 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
         if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
     }
     __syncthreads();
-    const uint64_t first = S.rpre[k0];
     const uint32_t total = cpre[kEmitRegions];
     for (uint32_t i = t; i < total; i += 256) {
         const uint64_t idx = first + i;
@@ -966,7 +1026,7 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
         const uint64_t base = (uint64_t)k * kRegion;
         const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
         const uint64_t pos = base + list[li];
-        const uint64_t next = li + 1 < c ? base + list[li + 1] : S.rexit[k];
+        const uint64_t next = li + 1 < c ? base + list[li + 1] : cex[r];
         offsets[idx] = pos + 16;
         lens[idx] = (uint32_t)(next - pos - 16);
     }

@@ -75,13 +75,15 @@ print(f"    candidate steps > 5: {(steps > 5).mean():6.1%}")
 # scan blocks (one row per block: start, states loaded, local fixes done, look-back done, end)
 y = y[y[:, 0] != 0]
 y[:, :5] -= t00
+y[:, 7] -= t00
 print(f"scan: {len(y)} blocks; first start {y[:, 0].min() / f:.1f} us after the first guess wave, "
       f"last end {y[:, 4].max() / f:.1f} us")
-ss = {"states loaded": y[:, 1] - y[:, 0], "local fixes": y[:, 2] - y[:, 1], "look-back": y[:, 3] - y[:, 2],
+ss = {"states loaded": y[:, 1] - y[:, 0], "first block composition": y[:, 7] - y[:, 1],
+      "local fixes": y[:, 2] - y[:, 1], "look-back": y[:, 3] - y[:, 2],
       "exact state + prefixes": y[:, 4] - y[:, 3], "block total": y[:, 4] - y[:, 0]}
 for k, v in ss.items():
     print(f"  {k:28s} median {np.median(v) / f:7.2f} us  p90 {np.percentile(v, 90) / f:7.2f} us  max {v.max() / f:7.2f} us")
 print(f"  blocks with fixes: {(y[:, 5] > 0).sum()} (regions re-walked {y[:, 5].sum()}); look-back retries "
       f"median {np.median(y[:, 6] & 0xFFFF):.0f} max {(y[:, 6] & 0xFFFF).max()}; first-seam waits max {(y[:, 6] >> 16).max()}")
-o_ = np.argsort(y[:, 7])
-print("  look-back done (us) by block:", " ".join(f"{v / f:.1f}" for v in y[o_, 3][:: max(1, len(y) // 16)]))
+o_ = np.argsort(y[:, 0])
+print("  look-back done (us) by start:", " ".join(f"{v / f:.1f}" for v in y[o_, 3][:: max(1, len(y) // 16)]))
