@@ -106,13 +106,18 @@ struct Agg {
     uint32_t bits;
 };
 __device__ __forceinline__ Agg agg_identity() { return Agg{0, 0, 0, kBitNone}; }
+// Without branches (selects; a "none" aggregate's first and cnt are 0): the scan steps, the
+// cross-wave loops and the look-back compose with no exec-mask save / restore per combine.
 __device__ __forceinline__ Agg combine(const Agg& a, const Agg& b) {
-    if (a.bits & kBitNone) {
-        if (b.bits & kBitNone) return Agg{0, a.last > b.last ? a.last : b.last, 0, kBitNone};
-        return b;
-    }
-    if (b.bits & kBitNone) return Agg{a.first, a.last, a.cnt, a.bits | (a.last < b.last ? kBitBad : 0u)};
-    return Agg{a.first, b.last, a.cnt + b.cnt, a.bits | b.bits | (a.last != b.first ? kBitBad : 0u)};
+    const bool an = (a.bits & kBitNone) != 0, bn = (b.bits & kBitNone) != 0;
+    Agg r;
+    r.first = an ? b.first : a.first;
+    r.last = an ? (bn ? (a.last > b.last ? a.last : b.last) : b.last) : (bn ? a.last : b.last);
+    r.cnt = a.cnt + b.cnt;
+    const uint32_t both = a.bits | b.bits | (a.last != b.first ? kBitBad : 0u);
+    const uint32_t abad = a.bits | (a.last < b.last ? kBitBad : 0u);
+    r.bits = an ? (bn ? kBitNone : b.bits) : (bn ? abad : both);
+    return r;
 }
 
 __device__ __forceinline__ uint32_t lane_id() {
@@ -633,12 +638,17 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
     __syncthreads();
     Agg before = agg_identity();
     int32_t ib = -1;
-    for (uint32_t q = 0; q < w; q++) {
-        before = combine(before, wtot[q]);
-        ib = widx[q] >= 0 ? widx[q] : ib;
-    }
     total = agg_identity();
-    for (uint32_t q = 0; q < (uint32_t)kWaves; q++) total = combine(total, wtot[q]);
+#pragma unroll
+    for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {  // the waves' totals in order (no loop branch)
+        const Agg wq = wtot[q];
+        const int32_t iq = widx[q];
+        if (q < w) {
+            before = combine(before, wq);
+            ib = iq >= 0 ? iq : ib;
+        }
+        total = combine(total, wq);
+    }
     // exclusive: the wave prefix before this lane
     Agg ex;
     int32_t iex;
