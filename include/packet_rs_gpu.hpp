@@ -176,6 +176,37 @@ class Parser {
         return r;
     }
 
+    // tests/pcap.rs:7-37 on the GPU: every record of a pcap capture in host memory through
+    // fast::parse_<entry> (pkt_parse_pcap_host: copy in, device index, parse, chain columns back).
+    // offsets[i] = record i's data offset in `file`, so BatchResult::slice(i, file + offsets[i]) is
+    // its PacketSlice.  Throws like the reference's unwrap on a malformed capture.
+    BatchResult parse_pcap(const uint8_t* file, size_t len, std::vector<uint64_t>& offsets,
+                           pkt_entry_t entry = PKT_ENTRY_PARSE) {
+        uint64_t n = 0;
+        check(pkt_pcap_index(file, len, nullptr, nullptr, 0, &n), nullptr, "pkt_pcap_index (malformed capture)");
+        BatchResult r;
+        r.n = n;
+        offsets.assign(n, 0);
+        if (n == 0) return r;
+        r.status.resize(n); r.n_hdrs.resize(n); r.hdr_type.resize(n * PKT_MAX_HDRS);
+        r.hdr_off.resize(n * PKT_MAX_HDRS); r.payload_off.resize(n); r.payload_len.resize(n);
+        r.hdr_mask.resize(n);
+        std::vector<uint32_t> lens(n);
+        pkt_out_t o;
+        std::memset(&o, 0, sizeof(o));
+        o.status = r.status.data();
+        o.n_hdrs = r.n_hdrs.data();
+        o.hdr_type = r.hdr_type.data();
+        o.hdr_off = r.hdr_off.data();
+        o.payload_off = r.payload_off.data();
+        o.payload_len = r.payload_len.data();
+        o.hdr_mask = r.hdr_mask.data();
+        uint64_t m = 0;
+        check(pkt_parse_pcap_host(ctx_, file, len, entry, &o, offsets.data(), lens.data(), n, &m), ctx_,
+              "pkt_parse_pcap_host");
+        return r;
+    }
+
    private:
     pkt_ctx_t* ctx_ = nullptr;
 };

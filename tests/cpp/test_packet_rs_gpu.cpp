@@ -53,8 +53,18 @@ int main(int argc, char** argv) {
         }
         std::printf("\n");
     }
+    // the same capture through Parser::parse_pcap (pkt_parse_pcap_host): identical chains and offsets
+    std::vector<uint64_t> poffs;
+    auto pres = parser.parse_pcap(buf.data(), buf.size(), poffs);
+    bool same = pres.n == n && poffs == offs && pres.status == res.status && pres.n_hdrs == res.n_hdrs &&
+                pres.payload_off == res.payload_off && pres.payload_len == res.payload_len;
+    for (uint64_t i = 0; same && i < n; i++)
+        for (int j = 0; j < res.n_hdrs[i]; j++)
+            same = same && pres.hdr_type[(uint64_t)j * n + i] == res.hdr_type[(uint64_t)j * n + i] &&
+                   pres.hdr_off[(uint64_t)j * n + i] == res.hdr_off[(uint64_t)j * n + i];
+    std::fprintf(stderr, "parse_pcap_equal %d\n", same ? 1 : 0);
     hipFree(d_slab);
     hipFree(d_offs);
     hipFree(d_lens);
-    return 0;
+    return same ? 0 : 4;
 }

@@ -26,8 +26,10 @@ def test_cpp_mirror_compiles():
 @pytest.mark.gpu
 def test_cpp_mirror_on_gpu():
     b = BIN if os.path.exists(BIN) else build()
-    out = subprocess.run([b, os.path.join(REPO, "tests", "golden", "ref22.pcap")], check=True,
-                         capture_output=True, text=True, timeout=120).stdout.strip().splitlines()
+    r = subprocess.run([b, os.path.join(REPO, "tests", "golden", "ref22.pcap")], check=True,
+                       capture_output=True, text=True, timeout=120)
+    assert "parse_pcap_equal 1" in r.stderr  # Parser::parse_pcap (pkt_parse_pcap_host) == parse_chain
+    out = r.stdout.strip().splitlines()
     exp = json.load(open(os.path.join(REPO, "tests", "golden", "ref22_expected.json")))
     assert len(out) == len(exp)
     for line, e in zip(out, exp):
