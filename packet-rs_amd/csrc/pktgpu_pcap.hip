@@ -605,7 +605,17 @@ __device__ __forceinline__ void scan_step(Agg& x, int32_t& ix) {
     ix = ix >= 0 ? ix : iy;
 }
 
-__device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, int32_t* widx, Agg& total) {
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t_;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t_;
+}
+
+// (bx: diagnostic stamps — after the wave scans, after the first barrier — or NULL)
+__device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, int32_t* widx, Agg& total,
+                                               uint64_t* bx = nullptr) {
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     int32_t ix = (a.bits & kBitNone) ? -1 : (int32_t)t;
     Agg x = a;
@@ -631,24 +641,30 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
         }
     }
     }
+    if (PKTGPU_STAMPS && bx) bx[0] = stamp_now();
     if (lane == 63) {
         wtot[w] = x;
         widx[w] = ix;
     }
     __syncthreads();
+    if (PKTGPU_STAMPS && bx) bx[1] = stamp_now();
+    // the waves' totals in order, one running composition (its value before wave w is this wave's
+    // prefix): four combines, no loop branch
     Agg before = agg_identity();
     int32_t ib = -1;
-    total = agg_identity();
+    Agg run = agg_identity();
+    int32_t irun = -1;
 #pragma unroll
-    for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {  // the waves' totals in order (no loop branch)
-        const Agg wq = wtot[q];
-        const int32_t iq = widx[q];
-        if (q < w) {
-            before = combine(before, wq);
-            ib = iq >= 0 ? iq : ib;
+    for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {
+        if (q == w) {
+            before = run;
+            ib = irun;
         }
-        total = combine(total, wq);
+        const int32_t iq = widx[q];
+        run = combine(run, wtot[q]);
+        irun = iq >= 0 ? iq : irun;
     }
+    total = run;
     // exclusive: the wave prefix before this lane
     Agg ex;
     int32_t iex;
@@ -705,6 +721,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     uint64_t st_[5] = {0, 0, 0, 0, 0};
     uint32_t n_fix = 0, n_wait = 0;
     uint64_t t_bx = 0;  // after the first block composition
+    uint64_t bx[2] = {0, 0};
 #endif
     PCAP_STAMP(0);
     // the block order: blockIdx when every block of the grid is resident at once (the host checks
@@ -782,7 +799,11 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     for (;;) {
         const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
         int32_t j;
+#if PKTGPU_STAMPS
+        const Agg pre = block_exclusive(mine, j, wtot, widx, total, t_bx ? nullptr : bx);
+#else
         const Agg pre = block_exclusive(mine, j, wtot, widx, total);
+#endif
 #if PKTGPU_STAMPS
         if (!t_bx) {
             __builtin_amdgcn_sched_barrier(0);
@@ -990,11 +1011,13 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     PCAP_STAMP(4);
     if (t == 0 && g_pcap_stamps) {  // after the guess kernel's K rows: one row per scan block
-        uint64_t* d = g_pcap_stamps + ((uint64_t)K + blk) * 8u;
+        uint64_t* d = g_pcap_stamps + (uint64_t)K * 8u + blk * 16u;
         for (int q = 0; q < 5; q++) d[q] = st_[q];
         d[5] = n_fix;
         d[6] = n_wait;
         d[7] = t_bx;
+        d[8] = bx[0];
+        d[9] = bx[1];
     }
 #endif
 }

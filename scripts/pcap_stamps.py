@@ -37,7 +37,7 @@ for _ in range(3):
     call()
 K = (buf.size + 4095) // 4096
 NB = (K + 255) // 256
-st = torch.zeros((K + NB) * 8, dtype=torch.uint64, device="cuda")
+st = torch.zeros(K * 8 + NB * 16, dtype=torch.uint64, device="cuda")
 D = ctypes.CDLL(os.environ["PKTGPU_LIB"])
 D.pkt_debug_pcap_stamps.argtypes = [ctypes.c_void_p]
 assert D.pkt_debug_pcap_stamps(ctypes.c_void_p(st.data_ptr())) == 0
@@ -46,9 +46,9 @@ call()
 torch.cuda.synchronize()
 D.pkt_debug_pcap_stamps(ctypes.c_void_p(0))
 assert cnt.value == n and np.array_equal(o.cpu().numpy(), offs)
-xa = st.cpu().numpy().view(np.int64).reshape(K + NB, 8)
-y = xa[K:].copy()
-x = xa[:K]
+xa = st.cpu().numpy().view(np.int64)
+y = xa[K * 8:].reshape(NB, 16).copy()
+x = xa[:K * 8].reshape(K, 8)
 x = x[x[:, 0] != 0].copy()
 t00 = x[:, 0].min()
 x[:, :5] -= t00  # one device-wide constant clock
@@ -76,9 +76,11 @@ print(f"    candidate steps > 5: {(steps > 5).mean():6.1%}")
 y = y[y[:, 0] != 0]
 y[:, :5] -= t00
 y[:, 7] -= t00
+y[:, 8:10] -= t00
 print(f"scan: {len(y)} blocks; first start {y[:, 0].min() / f:.1f} us after the first guess wave, "
       f"last end {y[:, 4].max() / f:.1f} us")
 ss = {"states loaded": y[:, 1] - y[:, 0], "first block composition": y[:, 7] - y[:, 1],
+      "  its wave scans": y[:, 8] - y[:, 1], "  its first barrier": y[:, 9] - y[:, 8],
       "local fixes": y[:, 2] - y[:, 1], "look-back": y[:, 3] - y[:, 2],
       "exact state + prefixes": y[:, 4] - y[:, 3], "block total": y[:, 4] - y[:, 0]}
 for k, v in ss.items():
