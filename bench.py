@@ -18,8 +18,10 @@ torch.distributed.run rank 0 is that process and the other ranks wait at a CPU (
 without touching a GPU.  The "c5" record times the C5 config through pkt_mgpu_parse_gather: 2^24
 packets in contiguous shards, parse and RCCL gather of the used tuple bytes to device 0 timed
 separately.
-At N = 1 the line also carries the host-memory rate ("host": pinned zero-copy pkt_parse_host) and
-the capture path ("pcap": capture in HBM -> pkt_pcap_index_device -> parse, one step).
+At N = 1 the line also carries the other device-resident BASELINE configs ("c3", "c4": each with its own
+roofline), the host-memory rate ("host": pinned zero-copy pkt_parse_host), the capture path ("pcap":
+capture in HBM -> pkt_pcap_index_device -> parse, one step; "pcap.index": the index kernels alone) and
+the capture in host memory ("host_pcap").
 
 Prints ONE JSON line (see DESIGN.md "Measurement" for every field).
 """
@@ -188,6 +190,9 @@ def load_probe():
     L.pkt_probe_ceiling.restype = ctypes.c_int
     L.pkt_probe_ceiling.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                     ctypes.POINTER(_lib.PktOut), ctypes.c_void_p]
+    L.pkt_probe_stream_copy.restype = ctypes.c_int
+    L.pkt_probe_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                                        ctypes.c_uint64, ctypes.c_void_p]
     L.pkt_probe_ceiling_groups.restype = ctypes.c_int
     L.pkt_probe_ceiling_groups.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                            ctypes.POINTER(_lib.PktOut), ctypes.c_void_p]
@@ -214,22 +219,23 @@ WORKLOAD = {"c2": "C2: 2^20 x 64 B Ether/IPv4/UDP fixed-stride slab per GPU",
             "c4": "C4: 2^20-record pcap replay of the 22 reference templates per GPU"}
 
 
-def roofline_phase(args, torch, P, batches, ostructs, raw_slabs, ring, n, stride, entry, default_cols, dev,
-                   slots):
+def roofline_phase(torch, P, cfg, use_probe, batches, ostructs, raw_slabs, ring, n, stride, entry, dev, slots, R,
+                   copy_args=None):
     """The parse kernel in isolation on device 0 — R back-to-back launches on ONE stream between one
     event pair on that stream — alternated with the ceiling probe (same launch shape, same bytes, no
-    parsing; the fixed-stride configs C2 and C3 with their default columns, `slots` header slot rows)
-    and a device copy of the slab.  Median of 5 rounds each."""
+    parsing; the fixed-stride configs C2 and C3 with their default columns, `slots` header slot rows),
+    a torch device copy of the slab and, for C2 (`copy_args` = (destination buffers, read bytes,
+    written bytes)), the hand-written streaming copy of the parse's bytes in one launch per batch and
+    in one launch over 16 batches (pkt_probe_stream_copy).  Median of 5 rounds each."""
     import ctypes
-    R = min(max(args.steps, 20), 50)
     rs = torch.cuda.Stream(dev)
-    probe = load_probe() if (args.config in ("c2", "c3", "c5") and args.columns == default_cols) else None
+    probe = load_probe() if use_probe else None
 
     def parse_launch(k, s):
         P.launch(batches[k % ring], entry, ostructs[k % ring], s)
 
     def probe_launch(k, s):
-        if args.config == "c3":
+        if cfg == "c3":
             rc = probe.pkt_probe_ceiling_groups(ctypes.c_void_p(raw_slabs[k % ring].data_ptr()), n, stride, slots,
                                                 ctypes.byref(ostructs[k % ring]), ctypes.c_void_p(s.cuda_stream))
         else:
@@ -244,22 +250,49 @@ def roofline_phase(args, torch, P, batches, ostructs, raw_slabs, ring, n, stride
         with torch.cuda.stream(s):
             copy_dst.copy_(raw_slabs[k % ring])
 
+    scopy = None
+    if probe is not None and copy_args is not None:
+        dsts, rb, wb = copy_args
+        kb = min(16, ring)
+        P8 = ctypes.POINTER(ctypes.c_uint8)
+
+        def ptrs(bufs):
+            return (P8 * len(bufs))(*[ctypes.cast(ctypes.c_void_p(b.data_ptr()), P8) for b in bufs])
+        srcs_all = [ptrs([raw_slabs[r]]) for r in range(ring)]
+        dsts_all = [ptrs([dsts[r]]) for r in range(ring)]
+        srcs_k, dsts_k = ptrs(raw_slabs[:kb]), ptrs(dsts[:kb])
+
+        def scopy_launch(k, s):
+            rc = probe.pkt_probe_stream_copy(srcs_all[k % ring], dsts_all[k % ring], 1, rb, wb,
+                                             ctypes.c_void_p(s.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"pkt_probe_stream_copy failed ({rc})")
+
+        def scopy_k_launch(k, s):
+            rc = probe.pkt_probe_stream_copy(srcs_k, dsts_k, kb, rb, wb, ctypes.c_void_p(s.cuda_stream))
+            if rc != 0:
+                raise RuntimeError(f"pkt_probe_stream_copy failed ({rc})")
+        scopy = {"one": [], "k": [], "kb": kb, "rb": rb, "wb": wb}
+
     kern, ceil_, copy_ = [], [], []
     for _ in range(5):
         kern.append(event_avg_ms(torch, rs, parse_launch, R))
         if probe is not None:
             ceil_.append(event_avg_ms(torch, rs, probe_launch, R))
         copy_.append(event_avg_ms(torch, rs, copy_launch, R))
+        if scopy is not None:
+            scopy["one"].append(event_avg_ms(torch, rs, scopy_launch, R))
+            scopy["k"].append(event_avg_ms(torch, rs, scopy_k_launch, max(4, R // 4)))
     del copy_dst
-    # the probe overwrote output sets: re-parse them so the outputs are real
+    # the probes overwrote output sets: re-parse them so the outputs are real
     for r in range(ring):
         parse_launch(r, rs)
     torch.cuda.synchronize(dev)
-    return R, kern, ceil_, copy_
+    return kern, ceil_, copy_, scopy
 
 
 def assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, slab_bytes, stride, offs_np, span,
-             pipe_s):
+             pipe_s, scopy=None):
     """The roofline / line-floor / traffic objects of the JSON line."""
     algo = read_b + write_b
     avg_kern_s = float(np.median(kern)) * 1e-3
@@ -286,6 +319,23 @@ def assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, s
             "avg_kernel_us": round(cs * 1e6, 3), "achieved": round(algo / cs / 1e9, 2),
             "frac_of_peak": round(algo / cs / 1e9 / HBM_PEAK_GBS, 4),
             "parse_frac_of_ceiling": round(cs / avg_kern_s, 4)}
+    if scopy is not None:
+        one_s = float(np.median(scopy["one"])) * 1e-3
+        k_s = float(np.median(scopy["k"])) * 1e-3 / scopy["kb"]
+        cb = scopy["rb"] + scopy["wb"]
+        res["roofline"]["ceiling"]["stream_copy"] = {
+            "kernel": "pkt_probe_stream_copy (libpktprobe.so): hand-written global_load_dwordx4 / "
+                      "global_store_dwordx4 copy, 1 KiB contiguous per wave instruction, 4 loads in flight "
+                      "per lane; the parse's read and written bytes, no parsing",
+            "read_bytes": scopy["rb"], "written_bytes": scopy["wb"],
+            "one_batch_per_launch": {"avg_kernel_us": round(one_s * 1e6, 3), "achieved": round(cb / one_s / 1e9, 2),
+                                     "frac_of_peak": round(cb / one_s / 1e9 / HBM_PEAK_GBS, 4),
+                                     "parse_frac_of_copy": round(one_s / avg_kern_s, 4)},
+            f"{scopy['kb']}_batches_per_launch": {"us_per_batch": round(k_s * 1e6, 3),
+                                                  "achieved": round(cb / k_s / 1e9, 2),
+                                                  "frac_of_peak": round(cb / k_s / 1e9 / HBM_PEAK_GBS, 4)},
+            "measured": f"median of 5 rounds, HIP events on one stream ({R} one-batch launches / "
+                        f"{max(4, R // 4)} {scopy['kb']}-batch launches per round), same ring as the parse"}
     # the line-granular floor: distinct 128-B lines holding header bytes + the batch index read
     # + the columns written, priced at this box's measured copy rate
     idx_b = 12 * n if offs_np is not None else 0
@@ -308,7 +358,7 @@ def assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, s
             "measured_in_this_run": False,
             "file": f"profiles/traffic_{args.config}.json",
             "how": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950) and WRITE_SIZE, separate passes of "
-                   "this bench command (scripts/gpu_round.sh)",
+                   f"bench.py --config {args.config} (scripts/gpu.sh traffic={args.config})",
             "x2_check": "every memory-side read request of these launches is a 128-B line "
                         "(TCC_EA0_RDREQ_128B = TCC_EA0_RDREQ; FETCH_SIZE counts 64 B per request): "
                         "profiles/ab/r02calib_fetch_requests.txt",
@@ -365,6 +415,23 @@ def pcap_record(P, torch, dev, n=1 << 20, reps=10):
         step()
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
+    # the index alone, its three kernels timed by HIP events between them (pkt_pcap_index_device_timed)
+    iw, ik = [], []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ci, ms = P.pcap_index_device_timed(d_buf, d_offs, d_lens, stream=s)
+        iw.append(time.perf_counter() - t0)
+        ik.append(ms)
+        ok = ok and ci == n
+    ik = np.median(np.array(ik), axis=0)
+    index = {"entry": "pkt_pcap_index_device_timed (blocking, cap = n: offsets and lens written)",
+             "ms_per_call": round(float(np.median(iw)) * 1e3, 4),
+             "kernel_us": {"guess": round(float(ik[0]) * 1e3, 2), "scan": round(float(ik[1]) * 1e3, 2),
+                           "emit": round(float(ik[2]) * 1e3, 2)},
+             "kernels_us_total": round(float(ik.sum()) * 1e3, 2),
+             "file_read_GB/s_guess": round(buf.size / (float(ik[0]) * 1e-3) / 1e9, 2),
+             "timing": "wall clock per blocking call and HIP events recorded between the kernels on the "
+                       "call's stream, median of reps"}
     # a stream of captures: pkt_parse_pcap_async on two ctxs / two streams, one capture in flight on
     # each, so one capture's index kernels overlap the other's parse (the C2 value's 2-stream form)
     import pktgpu
@@ -413,7 +480,7 @@ def pcap_record(P, torch, dev, n=1 << 20, reps=10):
                     "scan) + parse_kernel (all columns, record count read on the device); one blocking call",
             "ms_per_step": round(t * 1e3, 4), "Grecords/s": round(n / t / 1e9, 4),
             "file_GB/s": round(buf.size / t / 1e9, 2), "index_matches_host_indexer": bool(ok),
-            "reps": reps, "timing": "wall clock per step, median",
+            "reps": reps, "timing": "wall clock per step, median", "index": index,
             "pipelined": {"ms_per_capture": round(tp * 1e3, 4), "Grecords/s": round(n / tp / 1e9, 4),
                           "file_GB/s": round(buf.size / tp / 1e9, 2), "captures": K, "counts_ok": bool(ok_p),
                           "form": "pkt_parse_pcap_async on 2 ctxs x 2 streams, one capture in flight per ctx, "
@@ -561,8 +628,15 @@ def run_mgpu(args, ndev):
     ostructs0 = [P.out_struct(p0["outs"][r][1]) for r in range(ring)]
     o0 = p0["outs"][0][1]
     used_slots = int(o0["n_hdrs"].max().item()) if "n_hdrs" in o0 else 0
-    R, kern, ceil_, copy_ = roofline_phase(args, torch, P, batches0, ostructs0, p0["slabs"], ring, n, p0["stride"],
-                                           entry, default_cols, MP.torch_devices[0], used_slots)
+    R = min(max(args.steps, 20), 50)
+    default_shape = args.columns == default_cols
+    copy_args = None
+    if args.config == "c2" and default_shape:  # the streaming-copy ceiling of the C2 bytes
+        copy_args = ([p0["outs"][r][0] for r in range(ring)], p0["slab_np"].size,
+                     schema.bytes_per_packet(cols, n_slots=max(used_slots, 1)) * n)
+    kern, ceil_, copy_, scopy = roofline_phase(torch, P, args.config, args.config in ("c2", "c3", "c5") and default_shape,
+                                               batches0, ostructs0, p0["slabs"], ring, n, p0["stride"], entry,
+                                               MP.torch_devices[0], used_slots, R, copy_args)
 
     # ---------------- multi-batch launch (pkt_parse_batches): K ring batches in ONE launch, so the
     # launch's ramp and drain are paid once per K batches (same bytes per batch as `roofline`)
@@ -614,7 +688,7 @@ def run_mgpu(args, ndev):
                  "aggregate_frac_of_n_x_peak": round(agg_gbs / (ndev * HBM_PEAK_GBS), 4)},
     }
     assemble(args, res, n, ndev, cols, read_b, write_b, kern, ceil_, copy_, R, slab_bytes, p0["stride"],
-             p0["offs_np"], span, pipe_s)
+             p0["offs_np"], span, pipe_s, scopy)
     if batched is not None:
         bs = batched["us_per_batch"] * 1e-6
         batched.update({"achieved": round(algo / bs / 1e9, 2), "frac": round(algo / bs / 1e9 / HBM_PEAK_GBS, 4),
@@ -628,6 +702,10 @@ def run_mgpu(args, ndev):
                              "device = the same K steps re-issued between one HIP event pair on device 0"}
     if c5 is not None:
         res["c5"] = c5
+    if ndev == 1 and not args.no_extra and args.config == "c2":
+        # the other single-GPU BASELINE configs, device-resident, each with its own roofline
+        for cfg in ("c3", "c4"):
+            res[cfg] = config_record(args, torch, MP, P, cfg, entry)
     if ndev == 1 and not args.no_extra:
         res["host"] = host_record(P, torch, cols)
         res["pcap"] = pcap_record(P, torch, MP.torch_devices[0])
@@ -641,6 +719,83 @@ def run_mgpu(args, ndev):
     P.close()
     MP.close()
     return res
+
+
+def config_record(args, torch, MP, P, cfg, entry):
+    """A BASELINE config other than the headline's, device-resident on device 0 (N = 1 line): C3 (2^20 x
+    128 B Ether/{0-2}xVlan/IPv4/TCP|UDP, fast.rs:49-62, 203-207) or C4 (2^20-record capture of the 22
+    reference templates, fast.rs:5-227), with its default columns over its own >= ring_gib ring.  The
+    same measurements as the headline: K pipelined steps through pkt_mgpu_parse_steps (wall clock and
+    device-0 events), the isolated launch, the ceiling probe (C3) and the device copy of the slab (line
+    floor), 16 batches per launch (pkt_parse_batches), and the committed PMC traffic of the config."""
+    import pktgpu
+    from pktgpu import schema
+    cols_s = DEFAULT_COLS[cfg]
+    cols = pktgpu.resolve_columns("all" if cols_s == "all" else cols_s.split(","))
+    n = args.packets
+    dev = MP.torch_devices[0]
+    slab_np, stride, offs_np, lens_np = make_input(cfg, n, seed=0x5EED0000 + int(cfg[1:]))
+    ring = max(2, int(np.ceil(args.ring_gib * (1 << 30) / slab_np.size)))
+    first = torch.from_numpy(slab_np).to(dev)
+    slabs = [first] + [first.clone() for _ in range(ring - 1)]
+    offs = torch.from_numpy(offs_np).to(dev) if offs_np is not None else None
+    lens = torch.from_numpy(lens_np).to(dev) if lens_np is not None else None
+    outs = packed_outputs(torch, dev, cols, n, ring)
+    K, W = args.steps, args.warmup
+    plan = MP.steps_plan([[((slabs[k % ring], n, stride, offs, lens), outs[k % ring][0])] for k in range(W + K)])
+    if W:
+        MP.parse_steps(plan, entry, cols, first=0, count=W, streams=args.streams)
+    MP.synchronize()
+    timed = MP.steps_call(plan, entry, cols, first=W, count=K, streams=args.streams)
+    t0 = time.perf_counter()
+    timed()
+    MP.synchronize()
+    elapsed = time.perf_counter() - t0
+    ext0 = MP.streams()[0]
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(ext0)
+    timed()
+    e1.record(ext0)
+    MP.synchronize()
+    pipe_s = e0.elapsed_time(e1) * 1e-3 / K
+
+    batches = [P._batch(slabs[r], n, stride, offs, lens) for r in range(ring)]
+    ostructs = [P.out_struct(outs[r][1]) for r in range(ring)]
+    o0 = outs[0][1]
+    used_slots = int(o0["n_hdrs"].max().item())
+    R = min(max(K, 20), 50)
+    kern, ceil_, copy_, _ = roofline_phase(torch, P, cfg, cfg == "c3", batches, ostructs, slabs, ring, n, stride,
+                                           entry, dev, used_slots, R)
+    kb = min(16, ring)
+    rs = torch.cuda.Stream(dev)
+    call = P.batches_call(batches[:kb], ostructs[:kb], entry, rs)
+    bt = [event_avg_ms(torch, rs, lambda k, s: call(), max(4, min(R, 20))) for _ in range(5)]
+    span = o0["payload_off"].cpu().numpy()
+    ok = int((o0["status"] == 0).sum().item())
+    read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
+    algo = read_b + write_b
+    rec = {"workload": WORKLOAD[cfg], "entry": "fast::parse", "columns": cols_s, "packets": n,
+           "value": round(n * K / elapsed / 1e9, 4), "unit": "Gpkt/s", "steps": K, "warmup": W,
+           "ms_per_step": round(elapsed / K * 1e3, 5), "ring_slabs": ring, "ring_bytes": ring * slab_np.size,
+           "packets_status_ok": ok,
+           "launch": f"pkt_mgpu_parse_steps on device 0, {args.streams} streams (the headline's step form)",
+           "GB/s": {"algorithmic": round(algo * K / elapsed / 1e9, 2),
+                    "slab": round(slab_np.size * K / elapsed / 1e9, 2),
+                    "algorithmic_bytes_per_pkt": {"read": read_b / n, "written": write_b / n}}}
+    sub = argparse.Namespace(**vars(args))
+    sub.config, sub.columns = cfg, cols_s
+    assemble(sub, rec, n, 1, cols, read_b, write_b, kern, ceil_, copy_, R, slab_np.size, stride, offs_np, span,
+             pipe_s)
+    bs = float(np.median(bt)) * 1e-3 / kb
+    rec["roofline"]["kernel"] = "parse_kernel<6, 383u, 1> (lockstep walk, all columns)" if cfg == "c4" else \
+        "parse_kernel<4, 111u, 0> (waterfall walk + fast path)"
+    rec["roofline"]["batched"] = {"entry": "pkt_parse_batches", "batches_per_launch": kb, "packets_per_batch": n,
+                                  "us_per_batch": round(bs * 1e6, 3), "achieved": round(algo / bs / 1e9, 2),
+                                  "frac": round(algo / bs / 1e9 / HBM_PEAK_GBS, 4)}
+    del slabs, outs, batches, ostructs, first
+    torch.cuda.synchronize(dev)
+    torch.cuda.empty_cache()
+    return rec
 
 
 def run_c5_mgpu(args, torch, MP, per, cols, entry):
@@ -680,9 +835,13 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
     recv = torch.empty(MP.recv_bytes(one, cols, False), dtype=torch.uint8, device=MP.torch_devices[0])
     sh_out = [outs[i][0] for i in range(nd)]
 
-    def timed_gather(root_copy):
+    recv_m = torch.empty(MP.recv_bytes(one, cols, True), dtype=torch.uint8, device=MP.torch_devices[0])
+
+    def timed_gather(root_copy, merge=False, rows=0):
         MP.set_root_copy(root_copy)
-        MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)  # warm (RCCL channels)
+        MP.set_gather_rows(rows)
+        rb = recv_m if merge else recv
+        MP.parse_gather(one, columns=cols, merge=merge, shard_out=sh_out, recv=rb)  # warm (RCCL channels)
         MP.synchronize()
         tp, tg = [], []
         for _ in range(9):
@@ -691,20 +850,25 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
             MP.synchronize()
             tp.append(time.perf_counter() - t0)
             t0 = time.perf_counter()
-            MP.parse_gather(one, columns=cols, merge=False, shard_out=sh_out, recv=recv)
+            MP.parse_gather(one, columns=cols, merge=merge, shard_out=sh_out, recv=rb)
             MP.synchronize()
             tg.append(time.perf_counter() - t0)
         MP.set_root_copy(True)
+        MP.set_gather_rows(0)
         return float(np.median(tp)), float(np.median(tg)), max(min(tg) - min(tp), 1e-9)
 
     parse_s, pg_s, gmin_s = timed_gather(False)
     parse_c, pg_c, _ = timed_gather(True)
+    parse_m, pg_m, _ = timed_gather(False, merge=True)
     rows = int(max(int(o["n_hdrs"].max().item()) for o in
                    [mgpu.packed_views(sh_out[i], cols, one[i][1]) for i in range(nd)]))
+    parse_q, pg_q, _ = timed_gather(False, rows=rows)  # the caller's row bound: no host wait
     plan, _ = mgpu.gather_plan(cols, [sh[1] for sh in one], [rows] * nd, False)
+    plan_m, _ = mgpu.gather_plan(cols, [sh[1] for sh in one], [rows] * nd, True)
     moved = [sum(p[3] for p in plan if p[0] == i) for i in range(nd)]
     gather_s = max(pg_s - parse_s, 1e-9)
     gather_c = max(pg_c - parse_c, 1e-9)
+    gather_m = max(pg_m - parse_m, 1e-9)
     rec["gather"] = {"entry": "pkt_mgpu_parse_gather (merge = 0, root = device 0, pkt_mgpu_set_root_copy(0): "
                               "every shard's pieces, the root's own included, by grouped ncclSend/ncclRecv)",
                      "parse_ms": round(parse_s * 1e3, 4), "parse_plus_gather_ms": round(pg_s * 1e3, 4),
@@ -722,6 +886,15 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
                                    "parse_plus_gather_ms": round(pg_c * 1e3, 4),
                                    "what": "pkt_mgpu_set_root_copy(1), the default: the root's own pieces by "
                                            "hipMemcpyAsync on the root stream, the others by RCCL"},
+                     "merged": {"gather_ms": round(gather_m * 1e3, 4), "parse_plus_gather_ms": round(pg_m * 1e3, 4),
+                                "rccl_messages": len(plan), "repack_pieces": len(plan_m),
+                                "rccl_messages_if_sent_per_column": len(plan_m),
+                                "what": "merge = 1 (the whole batch's layout on the root), root copy off: the "
+                                        "merge = 0 messages into the root's staging area, then one repack "
+                                        "kernel placing every (shard, column / slot row) piece"},
+                     "queued": {"parse_plus_gather_ms": round(pg_q * 1e3, 4), "rows": rows,
+                                "what": "pkt_mgpu_set_gather_rows(rows): the caller's row bound, so parse and "
+                                        "gather are queued with no host wait (root copy off, merge = 0)"},
                      "timing": "wall clock around each blocking call (+ synchronize), median of 9 "
                                "(min: gather_min_ms); gather = (parse + gather) - parse; the call's slot-row count "
                                "is reduced inside the parse kernel and read back once per device"}

@@ -341,7 +341,12 @@ int pkt_extract_fields(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_chain
  * exactly as the reference's round trip reorders them.  `parsed` holds the chain columns of a
  * pkt_parse_batch over the same batch (status, n_hdrs, hdr_type, hdr_off, payload_off,
  * payload_len are read; the rest is ignored).  out_len[i] = bytes written (0 and nothing
- * written for a packet whose status is not PKT_OK); out_len may be NULL. */
+ * written for a packet whose status is not PKT_OK); out_len may be NULL.
+ * In the input's own layout (dst_offsets == NULL) of an indexed batch whose records share no
+ * 16-byte chunk of the slab (e.g. a capture, with its record headers between the packets), a
+ * destination chunk that holds a packet's first or last bytes is read, merged and written back
+ * whole: the dst bytes between records inside such a chunk are rewritten with their own values,
+ * not atomically — no other stream may write them while the call runs. */
 int pkt_to_vec_batch(pkt_ctx_t *ctx, const pkt_batch_t *batch, const pkt_out_t *parsed,
                      uint8_t *dst, uint64_t dst_len, const uint64_t *dst_offsets,
                      uint32_t *out_len, void *stream);
@@ -447,6 +452,11 @@ int pkt_pcap_index(const uint8_t *buf, uint64_t len, uint64_t *offsets, uint32_t
  * (pktgpu_pcap.hip).  Blocking: returns once *n_out is known (work is ordered on `stream`). */
 int pkt_pcap_index_device(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint64_t *offsets,
                           uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream);
+/* pkt_pcap_index_device with the index's three kernels timed by HIP events recorded between
+ * them on `stream` (measurement): kernel_ms[0..2] = guess, scan, emit (emit ~0 when cap == 0). */
+int pkt_pcap_index_device_timed(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, uint64_t *offsets,
+                                uint32_t *lens, uint64_t cap, uint64_t *n_out, void *stream,
+                                float *kernel_ms);
 
 /* The capture path of tests/pcap.rs:7-37 on a pcap file already in DEVICE memory, in one call:
  * pkt_pcap_index_device into offsets / lens (device, [cap], cap >= 1), then fast::parse_<entry> of
@@ -524,7 +534,8 @@ int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t *lo, uint64_t *hi);
  * `nshards` shards of n[i] packets whose batches use rows[i] (<= PKT_MAX_HDRS; rows NULL = all 16)
  * slot rows.  merge = 0: shard i's packed buffer (its used slot rows only, pkt_out_packed_pieces) at
  * the next 256-byte boundary of recv; merge = 1: recv is ONE packed output of sum(n) packets (each
- * column of shard i at packets [lo_i, lo_i + n_i), one piece per column and per used slot row).
+ * column of shard i at packets [lo_i, lo_i + n_i), one piece per column and per used slot row — the
+ * pieces the root's repack places after the merge = 0 transfer, see pkt_mgpu_parse_gather).
  * Writes min(cap, count) pieces, *npieces = count, *recv_bytes = the receive buffer size. */
 typedef struct pkt_gather_piece {
     uint64_t src;
@@ -570,17 +581,26 @@ int pkt_mgpu_parse_steps(pkt_mgpu_t *mg, const pkt_batch_t *batches, int steps, 
  * copies on the root's stream (an RCCL send to itself moved ~1 TB/s, the copy ~2 TB/s), 0 = RCCL
  * ncclSend / ncclRecv to itself inside the group like every other shard. */
 int pkt_mgpu_set_root_copy(pkt_mgpu_t *mg, int enable);
+/* Slot rows pkt_mgpu_parse_gather moves per shard: 0 (default) = each shard's largest n_hdrs, reduced
+ * inside its parse kernel — the host waits once per device for it before issuing the gather; 1..16 =
+ * that many rows for every shard (the caller's bound, >= every packet's n_hdrs; 16 always holds), so the
+ * parse and the gather are queued with no host wait at all. */
+int pkt_mgpu_set_gather_rows(pkt_mgpu_t *mg, int rows);
 /* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
  * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.
  * Grouped ncclSend/ncclRecv from the other devices; the root's own block per pkt_mgpu_set_root_copy. */
 int pkt_mgpu_gather(pkt_mgpu_t *mg, int root, const void *const *send, const uint64_t *bytes,
                     void *recv, uint64_t recv_len, const uint64_t *recv_off);
 /* pkt_mgpu_parse, then the gather of pkt_gather_plan(col_mask, ndev, n, rows, merge) into `recv` on
- * the root (recv_len >= its recv_bytes), where rows[i] = shard i's largest n_hdrs when n_hdrs is among
- * the columns (reduced inside each shard's parse kernel; the host waits once per device, after every
- * parse is queued), else all 16.  root_views (host array of ndev pkt_out_t, may be NULL) receives the
- * column pointers of each shard's tuples inside `recv` (merge = 0), or root_views[0] the single view
- * of the whole batch (merge = 1: what pkt_parse_batch over the whole batch would write). */
+ * the root (recv_len >= its recv_bytes with rows NULL), where rows[i] = pkt_mgpu_set_gather_rows' count,
+ * or by default shard i's largest n_hdrs when n_hdrs is among the columns (reduced inside each shard's
+ * parse kernel; the host waits once per device, after every parse is queued), else all 16.  merge = 0
+ * sends the plan's pieces as they are (<= 2 per shard).  merge = 1 sends the same <= 2 messages per
+ * shard into a staging area the handle keeps on the root, then one repack kernel on the root's stream
+ * places the merge = 1 plan's pieces (with the root copy on, the root's own pieces straight from its
+ * shard buffer).  root_views (host array of ndev pkt_out_t, may be NULL) receives the column pointers
+ * of each shard's tuples inside `recv` (merge = 0), or root_views[0] the single view of the whole batch
+ * (merge = 1: what pkt_parse_batch over the whole batch would write). */
 int pkt_mgpu_parse_gather(pkt_mgpu_t *mg, const pkt_batch_t *batches, int entry, uint64_t col_mask,
                           void *const *shard_out, int root, void *recv, uint64_t recv_len,
                           int merge, pkt_out_t *root_views);

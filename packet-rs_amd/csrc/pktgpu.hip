@@ -290,10 +290,38 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
-template <int NCH, uint32_t GM, int WK, bool STAGED = false, bool LATE = false>
+// ---- several batches in one launch (pkt_parse_batches) ----
+// K batches of the same size and layout whose outputs lie at one common byte distance from batch
+// 0's (e.g. one packed output buffer each): block j parses tile j % bpb of batch j / bpb.  Every
+// per-batch value comes from the kernel arguments (a scalar load at a computed offset: no table
+// read from memory before the block can start), and the launch's ramp and drain are paid once for
+// the K batches instead of once per batch.
+constexpr int kMaxMulti = 16;
+struct MultiBatch {
+    const uint8_t* slab;
+    uint64_t slab_len;
+    const uint64_t* offsets;
+    const uint32_t* lens;
+    int64_t out_delta;  // bytes from batch 0's column pointers to this batch's
+};
+struct MultiParams {
+    KParams base;  // batch 0 (its slab, index, outputs), the shared n / stride / entry / knobs
+    uint32_t bpb;  // blocks per batch
+    uint32_t k;
+    MultiBatch per[kMaxMulti];
+};
+static_assert(offsetof(MultiParams, base) == 0, "the late column loads read base.out at offsetof(KParams, out)");
+
+// Where the emit's column bases come from (LATE): L_EARLY = the KParams the kernel holds since its
+// start; L_SINGLE = loaded after the walk from the kernel arguments (parse_kernel: one KParams);
+// L_MULTI = the same from a MultiParams (its base.out) plus batch `mb`'s out_delta, also loaded after
+// the walk (parse_multi_kernel).
+enum LateCols : int { L_EARLY = 0, L_SINGLE = 1, L_MULTI = 2 };
+
+template <int NCH, uint32_t GM, int WK, bool STAGED = false, int LATE = L_EARLY>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T);
+                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T, uint32_t mb);
 
 // Dynamic LDS of a lockstep launch: the windows (or spans), then the dispatch tables.
 __host__ __device__ constexpr size_t with_tables(size_t bytes, int wk) {
@@ -319,9 +347,9 @@ __host__ __device__ constexpr int waves_per_eu(int nch, int wk) {
     return nch > 9 ? 1 : (wk == 1 && nch >= 6 ? (nch == 9 ? 4 : nch == 7 ? 5 : 6) : 8);
 }
 // Tile `blk` (256 packets) of the batch `p` describes: load, stage, walk, emit.
-template <int NCH, uint32_t GM, int WK, bool LATE = false>
+template <int NCH, uint32_t GM, int WK, int LATE = L_EARLY>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
-                                            uint64_t* pkt_st) {
+                                            uint64_t* pkt_st, uint32_t mb = 0) {
     const uint32_t base = blk * (uint32_t)kBlock;  // within this launch
     uint32_t n_eff = p.n;
     if (p.n_dev) {  // wave-uniform: the count the device produced (scalar load)
@@ -371,11 +399,11 @@ __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         PKT_STAMP(1);
-        parse_tile<NCH, GM, WK, true, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T);
+        parse_tile<NCH, GM, WK, true, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T, mb);
         return;
     }
     load_packet<NCH>(p, base + threadIdx.x, act, chunk, off, len);
-    parse_tile<NCH, GM, WK, false, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T);
+    parse_tile<NCH, GM, WK, false, LATE>(p, lds, base, chunk, off, len, act, pkt_st, T, mb);
 }
 
 template <int NCH, uint32_t GM, int WK>
@@ -385,30 +413,14 @@ void parse_kernel(KParams p) {
     uint64_t pkt_st[5] = {0, 0, 0, 0, 0};
     PKT_STAMP(0);
     const DispatchLds* T = tables<WK>(lds, window_lds(NCH), threadIdx.x, kBlock);
-    parse_block<NCH, GM, WK, PKTGPU_LATE_COLS != 0>(p, blockIdx.x, lds, T, pkt_st);
+    parse_block<NCH, GM, WK, PKTGPU_LATE_COLS != 0 ? L_SINGLE : L_EARLY>(p, blockIdx.x, lds, T, pkt_st);
 }
 
-// ---- several batches in one launch (pkt_parse_batches) ----
-// K batches of the same size and layout whose outputs lie at one common byte distance from batch
-// 0's (e.g. one packed output buffer each): block j parses tile j % bpb of batch j / bpb.  Every
-// per-batch value comes from the kernel arguments (a scalar load at a computed offset: no table
-// read from memory before the block can start), and the launch's ramp and drain are paid once for
-// the K batches instead of once per batch.
-constexpr int kMaxMulti = 16;
-struct MultiBatch {
-    const uint8_t* slab;
-    uint64_t slab_len;
-    const uint64_t* offsets;
-    const uint32_t* lens;
-    int64_t out_delta;  // bytes from batch 0's column pointers to this batch's
-};
-struct MultiParams {
-    KParams base;  // batch 0 (its slab, index, outputs), the shared n / stride / entry / knobs
-    uint32_t bpb;  // blocks per batch
-    uint32_t k;
-    MultiBatch per[kMaxMulti];
-};
-
+// Block j parses tile j % bpb of batch j / bpb.  Only the slot columns (hdr_type / hdr_off, which
+// the walk writes) are moved to the batch at the kernel start; the other 47 column bases and the
+// batch's out_delta are loaded after the walk (L_MULTI), as parse_kernel does: adding the delta to
+// all 49 bases up front held them through the walk and spilled 36 (C2 columns) / 42 (C4, all
+// columns) SGPRs to VGPR lanes (round-4 review).
 template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(waves_per_eu(NCH, WK))))
 void parse_multi_kernel(MultiParams mp) {
@@ -422,18 +434,17 @@ void parse_multi_kernel(MultiParams mp) {
     p.slab_len = mb.slab_len;
     p.offsets = mb.offsets;
     p.lens = mb.lens;
-    uint8_t** col = reinterpret_cast<uint8_t**>(&p.out);
-#pragma unroll
-    for (int c = 0; c < 49; c++)
-        if (col[c]) col[c] += mb.out_delta;
-    parse_block<NCH, GM, WK>(p, blockIdx.x - b * mp.bpb, lds, T, pkt_st);
+    if (p.out.hdr_type) p.out.hdr_type += mb.out_delta;
+    if (p.out.hdr_off) p.out.hdr_off = reinterpret_cast<uint16_t*>(reinterpret_cast<uint8_t*>(p.out.hdr_off) + mb.out_delta);
+    parse_block<NCH, GM, WK, L_MULTI>(p, blockIdx.x - b * mp.bpb, lds, T, pkt_st, b);
 }
 
-template <int NCH, uint32_t GM, int WK, bool STAGED, bool LATE>
+template <int NCH, uint32_t GM, int WK, bool STAGED, int LATE>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
-                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T) {
+                                           bool active_own, uint64_t* pkt_st, const DispatchLds* T, uint32_t mb) {
     (void)pkt_st;
+    (void)mb;
     const uint32_t t = threadIdx.x;
     const uint32_t i_own = base + t;
     // Register fast path (pkt_ctx_set_fastpath): an aligned packet whose EtherType chain is
@@ -513,7 +524,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         if ((t & 63u) == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
     if (active_own) {
-        if constexpr (LATE) {
+        if constexpr (LATE != L_EARLY) {
             // The column bases are loaded here, after the walk, by scalar loads from the kernel
             // arguments (an opaque copy of their address keeps the loads from being hoisted to the
             // kernel start), and re-marked as global pointers so every store stays a global store.
@@ -521,14 +532,29 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
             // through the walk and spilled 48 to VGPR lanes (~96 lane instructions per wave); round
             // 3's late load through a generic pointer made every column access a flat access, 6x
             // slower (profiles/ab/r03j_late_column_pointers.txt).
-            // (parse_kernel's only argument is the KParams: it starts the kernarg segment)
-            uint64_t ka = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(KParams, out);
+            // (parse_kernel's only argument is the KParams, parse_multi_kernel's the MultiParams
+            // whose first member is batch 0's KParams: either starts the kernarg segment)
+            const uint64_t kseg = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+            uint64_t ka = kseg + offsetof(KParams, out);
             asm volatile("" : "+s"(ka));
             const void* const KARG_AS* kc = reinterpret_cast<const void* const KARG_AS*>(ka);
+            int64_t delta = 0;
+            if constexpr (LATE == L_MULTI) {
+                // (mb is wave-uniform, but the integer division that made it leaves it in a VGPR)
+                const uint32_t mbs = __builtin_amdgcn_readfirstlane(mb);
+                uint64_t kd = kseg + offsetof(MultiParams, per) + (uint64_t)mbs * sizeof(MultiBatch) +
+                              offsetof(MultiBatch, out_delta);
+                asm volatile("" : "+s"(kd));
+                delta = *reinterpret_cast<const int64_t KARG_AS*>(kd);
+            }
             pkt_out_t oc;
             void** ocp = reinterpret_cast<void**>(&oc);
 #pragma unroll
-            for (int c = 0; c < 49; c++) ocp[c] = as_global(const_cast<void*>(kc[c]));
+            for (int c = 0; c < 49; c++) {
+                const void* q = kc[c];
+                if constexpr (LATE == L_MULTI) q = q ? reinterpret_cast<const uint8_t*>(q) + delta : q;
+                ocp[c] = as_global(const_cast<void*>(q));
+            }
             emit_chain<GM>(oc, i_own, len_own, r);
             emit_fields<GM>(oc, i_own, pv_own, r, r.status == PKT_OK);
         } else {
@@ -580,18 +606,20 @@ template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x;
-    const DispatchLds* T = tables<WK>(lds, span_region(NCH), lane, kSpanBlock);
-    const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
     uint32_t n_eff = p.n;
-    if (p.n_dev) {
+    if (p.n_dev) {  // wave-uniform: the count the device produced (scalar load)
         const uint64_t nd = *p.n_dev;
         n_eff = nd < (uint64_t)n_eff ? (uint32_t)nd : n_eff;
+        if (blockIdx.x * kSpanBlock >= n_eff) return;  // the whole wave (= block) is past the count
     }
+    const DispatchLds* T = tables<WK>(lds, span_region(NCH), lane, kSpanBlock);
+    const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
     const bool active = i < n_eff;
     uint64_t off = 0;
     uint32_t len = 0;
     if (active) packet_range(p, i, off, len);
-    // the wave's byte range [lo, hi) (butterfly min/max; lane 0 is always active)
+    // the wave's byte range [lo, hi) (butterfly min/max; lane 0 is active: blocks whose first packet
+    // lies past the count have returned above)
     uint64_t lo = active ? off : ~(uint64_t)0, hi = active ? off + len : 0;
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1) {
@@ -854,6 +882,8 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         (void)hipSetDevice(ctx->device);
         (void)hipDeviceSynchronize();
         (void)hipFree(ctx->tv_flag);
+        for (hipEvent_t ev : ctx->tv_ev)
+            if (ev) (void)hipEventDestroy(ev);
     }
     if (ctx && ctx->mx.dev) {
         (void)hipSetDevice(ctx->device);
@@ -948,6 +978,10 @@ int pkt_parse_batches(pkt_ctx_t* ctx, const pkt_batch_t* batches, uint32_t nbatc
             delta = d;
             have = true;
         }
+        // batch k's IPv6 address columns are batch 0's + delta: the 16-byte alignment parse_impl
+        // checks for batch 0 holds for every batch only if delta keeps it (else one call per batch,
+        // each validated)
+        if ((c0[kColIpv6Src] || c0[kColIpv6Dst]) && (delta & 15) != 0) one = false;
         if (one) mp.per[k] = MultiBatch{b.slab, b.slab_len, b.offsets, b.lens, delta};
     }
     if (!one) {
@@ -1358,7 +1392,10 @@ int pkt_parse_pcap_host_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, 
     hipError_t e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)");
     const uint64_t* count_dev = nullptr;
-    if ((rc = pktgpu_pcap_launch(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, s, &count_dev)) != PKT_SUCCESS) return rc;
+    if ((rc = pktgpu_pcap_launch(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, s, &count_dev)) != PKT_SUCCESS) {
+        (void)hipStreamSynchronize(s);  // the copy queued above may still be reading `buf`
+        return rc;
+    }
     pkt_batch_t db;
     db.slab = hp.file;
     db.slab_len = len;
@@ -1392,19 +1429,26 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
     hipStream_t s = hp.s[0];
+    // every error return after the first queued copy waits for the ctx's streams first: a copy from
+    // `buf` or into `offsets` / `lens` must not outlive the call
+    auto bail = [&](int code) {
+        (void)hipStreamSynchronize(hp.s[0]);
+        (void)hipStreamSynchronize(hp.s[1]);
+        return code;
+    };
     // in: the whole file, one copy (the record chain is sequential: the index needs all of it)
     if ((e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s)) != hipSuccess)
-        return hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)");
+        return bail(hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)"));
     uint64_t n = 0;
     rc = pkt_pcap_index_device(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, &n, s);
-    if (rc != PKT_SUCCESS) return rc;
+    if (rc != PKT_SUCCESS) return bail(rc);
     *n_out = n;
     const uint64_t m = std::min(n, cap);
     if (m == 0) return PKT_SUCCESS;
     if (offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
-        return hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)");
+        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)"));
     if (lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
-        return hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)");
+        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)"));
     pkt_batch_t db;
     db.slab = hp.file;
     db.slab_len = len;
@@ -1418,13 +1462,13 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
     pkt_out_t dout;
     if (out_mapped(out, dout)) {
         rc = parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap);
-        if (rc != PKT_SUCCESS) return rc;
+        if (rc != PKT_SUCCESS) return bail(rc);
         for (int k = 0; k < 2; k++)
             if ((e = hipStreamSynchronize(hp.s[k])) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
         return PKT_SUCCESS;
     }
     rc = staged_parse(ctx, &db, entry, out, 0, true, cap);
-    if (rc != PKT_SUCCESS) return rc;
+    if (rc != PKT_SUCCESS) return bail(rc);
     if ((e = hipStreamSynchronize(hp.s[1])) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
     return PKT_SUCCESS;
 }

@@ -49,6 +49,8 @@ constexpr uint8_t kColSize[kNumCols] = {1, 1, 1, 2, 2, 2, 4, 8, 8, 2, 1, 1, 2, 2
                                         1, 1, 2, 4, 4, 2, 1, 1, 4, 2, 1, 1, 16, 16, 2, 2, 4, 4, 1,
                                         1, 1, 2, 2, 2, 2, 2, 2, 2};
 constexpr int kColHdrType = 2, kColHdrOff = 3;  // slot-major [PKT_MAX_HDRS][n]
+constexpr int kColIpv6Src = 33, kColIpv6Dst = 34;  // 16 raw bytes per packet, 16-byte aligned
+static_assert(kColSize[kColIpv6Src] == 16 && kColSize[kColIpv6Dst] == 16, "ipv6 address columns");
 static_assert(sizeof(pkt_out_t) == kNumCols * sizeof(void*), "pkt_out_t layout");
 
 // Bytes of column c for n packets.
@@ -83,9 +85,11 @@ struct pkt_ctx {
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
     // pkt_to_vec_batch: device words, nonzero = a chunk holds bytes of two records; a ring, one word
-    // per call, so calls in flight on several streams never share one
+    // per call, so calls in flight on several streams do not share one; a word is reused only after
+    // the call that last used it has passed its to_vec kernel (the call's stream waits on tv_ev[k])
     static constexpr uint32_t kTvFlags = 256;
     uint32_t* tv_flag = nullptr;
+    hipEvent_t tv_ev[kTvFlags] = {};
     uint32_t tv_next = 0;
     std::string err;
 };
@@ -120,3 +124,13 @@ int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
                        uint64_t cap, hipStream_t s, const uint64_t** count_dev);
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out);
 int pktgpu_pcap_take(pkt_ctx_t* ctx, uint64_t* n_out);  // a queued capture's outcome (waits; clears pending)
+
+// The merged gather's root-side repack (pktgpu_gather.hip): copy `bytes` from device address `src` to
+// `dst` for every piece; piece p is served by blocks [first_block, first_block + pktgpu_repack_blocks(
+// bytes)), the table sorted by first_block (used by pkt_mgpu_parse_gather, pktgpu_mgpu.cpp).
+struct RepackPiece {
+    uint64_t src, dst, bytes;
+    uint32_t first_block, reserved;
+};
+uint32_t pktgpu_repack_blocks(uint64_t bytes);
+hipError_t pktgpu_repack_launch(const RepackPiece* tab_dev, uint32_t np, uint32_t nblocks, hipStream_t s);

@@ -30,6 +30,16 @@ struct pkt_mgpu {
     std::vector<hipEvent_t> xe;   // [ndev][kMaxStreams]
     bool xinit = false;           // xs / xe all created (set only after every creation succeeded)
     int root_copy = 1;            // the root's own pieces: 1 = hipMemcpyAsync, 0 = RCCL send/recv to itself
+    int gather_rows = 0;          // slot rows parse_gather moves: 0 = each shard's largest n_hdrs (waits), 1..16 fixed
+    // merge = 1: the root's staging area for the shards' packed buffers (the merge = 0 transfer) and
+    // the repack table (pinned host copy, device copy; rp_ev = the last table upload has been read)
+    int stage_dev = -1;
+    uint8_t* stage = nullptr;
+    uint64_t stage_cap = 0;
+    RepackPiece* rp_host = nullptr;
+    RepackPiece* rp_dev = nullptr;
+    uint64_t rp_cap = 0;  // pieces
+    hipEvent_t rp_ev = nullptr;
     std::string err;
 };
 
@@ -250,6 +260,13 @@ int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
             }
         for (size_t k = i * pkt_mgpu::kMaxStreams; k < mg->xe.size() && k < (i + 1) * (size_t)pkt_mgpu::kMaxStreams; k++)
             if (mg->xe[k]) (void)hipEventDestroy(mg->xe[k]);
+        if (mg->dev[i] == mg->stage_dev) {
+            (void)hipDeviceSynchronize();
+            (void)hipFree(mg->stage);
+            (void)hipFree(mg->rp_dev);
+            (void)hipHostFree(mg->rp_host);
+            if (mg->rp_ev) (void)hipEventDestroy(mg->rp_ev);
+        }
         if (mg->comm[i]) (void)ncclCommDestroy(mg->comm[i]);
         if (mg->stream[i]) (void)hipStreamDestroy(mg->stream[i]);
         if (mg->ctx[i]) pkt_ctx_destroy(mg->ctx[i]);
@@ -388,6 +405,12 @@ int pkt_mgpu_set_root_copy(pkt_mgpu_t* mg, int enable) {
     return PKT_SUCCESS;
 }
 
+int pkt_mgpu_set_gather_rows(pkt_mgpu_t* mg, int rows) {
+    if (!mg || rows < 0 || rows > PKT_MAX_HDRS) return mfail(mg, PKT_ERR_INVALID_ARG, "bad argument");
+    mg->gather_rows = rows;
+    return PKT_SUCCESS;
+}
+
 }  // extern "C"
 
 namespace {
@@ -417,6 +440,97 @@ int issue_plan(pkt_mgpu* mg, int root, const void* const* send, void* recv, cons
     const ncclResult_t r2 = ncclGroupEnd();
     if (r != ncclSuccess) return mnccl(mg, r, "ncclSend/ncclRecv");
     if (r2 != ncclSuccess) return mnccl(mg, r2, "ncclGroupEnd");
+    return PKT_SUCCESS;
+}
+
+// The merged gather (merge = 1): the shards' packed buffers move as in merge = 0 (<= 2 messages per
+// shard, their used slot rows only) into the root's staging area, then one repack kernel on the root
+// stream places each piece of `pieces` (pkt_gather_plan's merge = 1 plan: source offset in the shard's
+// packed buffer, destination offset in recv) — 16 messages instead of 248 for C2 at 8 x 2^21.  With
+// the root copy on, the root's own pieces are repacked straight from its shard buffer (no staging).
+int merged_gather(pkt_mgpu* mg, int root, const void* const* shard_out, void* recv, const std::vector<uint64_t>& n,
+                  const std::vector<uint32_t>& rows, uint64_t mask, const std::vector<pkt_gather_piece_t>& pieces) {
+    const int nd = mg->ndev;
+    std::vector<pkt_gather_piece_t> msgs;
+    const uint64_t stage_need = gather_plan(mask, nd, n.data(), rows.data(), 0, msgs);
+    // each shard's packed buffer sits at stage + its merge = 0 offset (the same loop as gather_plan)
+    std::vector<uint64_t> sofs(nd, 0);
+    uint64_t need = 0;
+    for (int i = 0; i < nd; i++) {
+        sofs[i] = round_up(need);
+        need = sofs[i] + packed_layout(mask, n[i], nullptr);
+    }
+    hipError_t e = hipSetDevice(mg->dev[root]);
+    if (e != hipSuccess) return mhip(mg, e, "hipSetDevice (root)");
+    if (mg->stage_dev != -1 && mg->stage_dev != mg->dev[root]) {  // a new root device: drop the old buffers
+        (void)hipSetDevice(mg->stage_dev);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(mg->stage);
+        (void)hipFree(mg->rp_dev);
+        (void)hipHostFree(mg->rp_host);
+        if (mg->rp_ev) (void)hipEventDestroy(mg->rp_ev);
+        mg->stage = nullptr;
+        mg->rp_dev = mg->rp_host = nullptr;
+        mg->rp_ev = nullptr;
+        mg->stage_cap = mg->rp_cap = 0;
+        if ((e = hipSetDevice(mg->dev[root])) != hipSuccess) return mhip(mg, e, "hipSetDevice (root)");
+    }
+    mg->stage_dev = mg->dev[root];
+    if (!mg->rp_ev && (e = hipEventCreateWithFlags(&mg->rp_ev, hipEventDisableTiming)) != hipSuccess)
+        return mhip(mg, e, "hipEventCreate (repack)");
+    const bool staged_any = std::any_of(msgs.begin(), msgs.end(),
+                                        [&](const pkt_gather_piece_t& p) { return p.shard != root || !mg->root_copy; });
+    if (staged_any && stage_need > mg->stage_cap) {
+        if ((e = hipStreamSynchronize(mg->stream[root])) != hipSuccess) return mhip(mg, e, "hipStreamSynchronize");
+        (void)hipFree(mg->stage);
+        mg->stage = nullptr;
+        mg->stage_cap = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&mg->stage), stage_need)) != hipSuccess)
+            return mhip(mg, e, "hipMalloc (gather staging)");
+        mg->stage_cap = stage_need;
+    }
+    if (pieces.size() > mg->rp_cap) {
+        if ((e = hipEventSynchronize(mg->rp_ev)) != hipSuccess) return mhip(mg, e, "hipEventSynchronize");
+        (void)hipFree(mg->rp_dev);
+        (void)hipHostFree(mg->rp_host);
+        mg->rp_dev = mg->rp_host = nullptr;
+        mg->rp_cap = 0;
+        const uint64_t cap = pieces.size() + 64;
+        e = hipMalloc(reinterpret_cast<void**>(&mg->rp_dev), cap * sizeof(RepackPiece));
+        if (e == hipSuccess) e = hipHostMalloc(reinterpret_cast<void**>(&mg->rp_host), cap * sizeof(RepackPiece), hipHostMallocDefault);
+        if (e != hipSuccess) return mhip(mg, e, "hipMalloc (repack table)");
+        mg->rp_cap = cap;
+    }
+    // the transfer: the merge = 0 messages into the staging area, the root's own skipped with the
+    // root copy on (repacked from its shard buffer below)
+    std::vector<pkt_gather_piece_t> sent;
+    for (const pkt_gather_piece_t& p : msgs)
+        if (p.shard != root || !mg->root_copy) sent.push_back(p);
+    if (!sent.empty()) {
+        const int keep = mg->root_copy;
+        mg->root_copy = 0;  // issue_plan: every listed piece by RCCL (the root's own only when listed)
+        const int rc = issue_plan(mg, root, shard_out, mg->stage, sent);
+        mg->root_copy = keep;
+        if (rc != PKT_SUCCESS) return rc;
+    }
+    // the repack table: absolute device addresses, block ranges in table order
+    if ((e = hipEventSynchronize(mg->rp_ev)) != hipSuccess) return mhip(mg, e, "hipEventSynchronize (repack table)");
+    uint32_t blocks = 0;
+    uint32_t np = 0;
+    for (const pkt_gather_piece_t& p : pieces) {
+        if (!p.bytes) continue;
+        const bool direct = p.shard == root && mg->root_copy;
+        const uint8_t* src = direct ? static_cast<const uint8_t*>(shard_out[root]) + p.src : mg->stage + sofs[p.shard] + p.src;
+        mg->rp_host[np++] = RepackPiece{reinterpret_cast<uint64_t>(src), reinterpret_cast<uint64_t>(recv) + p.dst, p.bytes,
+                                        blocks, 0u};
+        blocks += pktgpu_repack_blocks(p.bytes);
+    }
+    if (!np) return PKT_SUCCESS;
+    hipStream_t rs = mg->stream[root];
+    if ((e = hipMemcpyAsync(mg->rp_dev, mg->rp_host, np * sizeof(RepackPiece), hipMemcpyHostToDevice, rs)) != hipSuccess)
+        return mhip(mg, e, "hipMemcpyAsync (repack table)");
+    if ((e = hipEventRecord(mg->rp_ev, rs)) != hipSuccess) return mhip(mg, e, "hipEventRecord (repack table)");
+    if ((e = pktgpu_repack_launch(mg->rp_dev, np, blocks, rs)) != hipSuccess) return mhip(mg, e, "repack_kernel");
     return PKT_SUCCESS;
 }
 }  // namespace
@@ -463,8 +577,9 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
     // nothing, a PacketSlice holds exactly its headers): reduced inside the parse kernel and copied
     // to pinned host memory on the shard's stream; the host waits once per device, after every
     // shard's parse is queued.
-    const bool nh = mask >> 1 & 1;
-    std::vector<uint32_t> rows(nd, PKT_MAX_HDRS);
+    // with a fixed row count (pkt_mgpu_set_gather_rows) nothing is measured and the host never waits
+    const bool nh = (mask >> 1 & 1) && mg->gather_rows == 0;
+    std::vector<uint32_t> rows(nd, mg->gather_rows ? (uint32_t)mg->gather_rows : PKT_MAX_HDRS);
     std::vector<const uint32_t*> rows_host(nd, nullptr);
     for (int i = 0; i < nd; i++) {
         if (!n[i]) continue;
@@ -485,8 +600,8 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
             for (int k = 0; k < MaxScratch::kSpread; k++) m = std::max(m, rows_host[i][k]);
             rows[i] = std::min<uint32_t>(m, PKT_MAX_HDRS);
         }
-        gather_plan(mask, nd, n.data(), rows.data(), merge, plan);
     }
+    if (nh || mg->gather_rows) gather_plan(mask, nd, n.data(), rows.data(), merge, plan);
     if (root_views) {
         if (merge) {
             pkt_out_packed(mask, n_total, recv, &root_views[0], nullptr);
@@ -499,7 +614,8 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
             }
         }
     }
-    return issue_plan(mg, root, shard_out, recv, plan);
+    if (!merge) return issue_plan(mg, root, shard_out, recv, plan);
+    return merged_gather(mg, root, shard_out, recv, n, rows, mask, plan);
 }
 
 int pkt_mgpu_synchronize(pkt_mgpu_t* mg) {

@@ -724,8 +724,10 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     uint64_t bx[2] = {0, 0};
 #endif
     PCAP_STAMP(0);
-    // the block order: blockIdx when every block of the grid is resident at once (the host checks
-    // the occupancy), else a ticket (every lower block is then already running)
+    // the block order: blockIdx when the device could hold the whole grid at once (the host checks
+    // the occupancy; progress then rests on the dispatcher launching workgroups in blockIdx order, so
+    // every lower block has been dispatched before this one — see pcap_launch), else a ticket (every
+    // lower ticket's block is then already running)
     if (t == 0) s_blk = ticket ? atomicAdd(S.ticket, 1u) : blockIdx.x;
     __syncthreads();
     const uint32_t blk = s_blk;
@@ -1071,8 +1073,10 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
 // Queue the index of the pcap file `buf` on `s` (guess + scan kernels; the scan writes the records):
 // no host synchronisation.  *count_dev = the device word a following parse may take its record count
 // from (0 after an error).  pcap_finish reads the outcome once the stream is synchronised.
+// ev (measurement only, pkt_pcap_index_device_timed): 4 events recorded on `s` before the guess
+// kernel and after each of the three kernels.
 static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                       uint64_t cap, hipStream_t s, const uint64_t** count_dev) {
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, hipEvent_t* ev = nullptr) {
     if (!ctx || !buf || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
@@ -1136,7 +1140,9 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     S.epoch = pc.epoch;
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
+    if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
+    if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     if (!pc.scan_resident) {  // scan blocks the device holds at once
         int per_cu = 0, cus = 0;
         if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_scan_kernel, 256, 0) != hipSuccess ||
@@ -1145,11 +1151,18 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
         pc.scan_resident = (uint32_t)std::max(1, per_cu * cus);
     }
     // (tickets serialise: 186 device-scope atomics on one word cost the last block ~2.4 us)
+    // Forward progress of the blockIdx-ordered look-back: a running block waits only for blocks of
+    // LOWER blockIdx, and the dispatcher launches a kernel's workgroups in blockIdx order, so every
+    // such block has been dispatched (is resident or finished) — whatever else occupies the device,
+    // e.g. the other ctx's capture of the async entries.  The occupancy test keeps the ticket for a
+    // grid the device could not hold at once even alone.
     hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
+    if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
     if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
+    if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
     if (count_dev) *count_dev = S.dev;
@@ -1203,6 +1216,29 @@ int pkt_pcap_index_device(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint
     const hipError_t e = hipStreamSynchronize(s);
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index");
     return pcap_finish(ctx, n_out);
+}
+
+int pkt_pcap_index_device_timed(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
+                                uint64_t cap, uint64_t* n_out, void* stream, float* kernel_ms) {
+    if (!ctx || !n_out || !kernel_ms) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
+    *n_out = 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
+    hipEvent_t ev[4] = {};
+    for (int k = 0; k < 4 && e == hipSuccess; k++) e = hipEventCreate(&ev[k]);
+    int rc = e == hipSuccess ? pcap_launch(ctx, buf, len, offsets, lens, cap, s, nullptr, ev) : hip_fail(ctx, e, "hipEventCreate");
+    if (rc == PKT_SUCCESS) {
+        if ((e = hipStreamSynchronize(s)) != hipSuccess) rc = hip_fail(ctx, e, "pcap index");
+        for (int k = 0; k < 3 && rc == PKT_SUCCESS; k++)
+            if ((e = hipEventElapsedTime(&kernel_ms[k], ev[k], ev[k + 1])) != hipSuccess) rc = hip_fail(ctx, e, "hipEventElapsedTime");
+        if (rc == PKT_SUCCESS) rc = pcap_finish(ctx, n_out);
+    } else {
+        (void)hipStreamSynchronize(s);
+    }
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    return rc;
 }
 
 // The index kernels and the counted parse, queued on `stream` (no host wait).

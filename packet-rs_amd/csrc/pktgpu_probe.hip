@@ -224,3 +224,60 @@ extern "C" int pkt_probe_c4load(const uint8_t* slab, uint64_t slab_len, const ui
                        slab_len, offs, n, nch, align_log2, out);
     return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
 }
+
+// pkt_probe_stream_copy: the streaming-copy ceiling of the C2 roofline (bench.py roofline.ceiling
+// .stream_copy).  A hand-written copy with the parse's BYTES but the ideal access shape: batch b
+// reads read_bytes from srcs[b] and writes write_bytes to dsts[b] (the chunks past read_bytes are
+// derived from their index), every access a 16-byte global_load_dwordx4 / global_store_dwordx4 by
+// consecutive lanes (1 KiB contiguous per wave instruction), four loads in flight per lane before
+// the first store.  k batches in one launch (block j serves batch j / bpb), so the k = 1 launch and
+// the k = 16 launch are the copy forms of the parse's one-batch and pkt_parse_batches launches.
+namespace {
+constexpr int kCopyMax = 16;
+constexpr uint32_t kCopyU = 4;  // 16-byte chunks per lane
+struct CopyArgs {
+    const uint4* src[kCopyMax];
+    uint4* dst[kCopyMax];
+    uint64_t nr, nw;  // 16-byte chunks read / written per batch
+    uint32_t bpb;     // blocks per batch
+};
+__global__ __launch_bounds__(256) void stream_copy_kernel(CopyArgs a) {
+    const uint32_t b = blockIdx.x / a.bpb;
+    const uint64_t c0 = (uint64_t)(blockIdx.x - b * a.bpb) * (256u * kCopyU) + threadIdx.x;
+    const uint4* __restrict__ s = a.src[b];
+    uint4* __restrict__ d = a.dst[b];
+    uint4 v[kCopyU];
+#pragma unroll
+    for (uint32_t u = 0; u < kCopyU; u++) {
+        const uint64_t c = c0 + 256u * u;
+        v[u] = c < a.nr ? s[c] : make_uint4((uint32_t)c, (uint32_t)(c >> 32), 0u, 0u);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kCopyU; u++) {
+        const uint64_t c = c0 + 256u * u;
+        if (c < a.nw) d[c] = v[u];
+    }
+}
+}  // namespace
+
+extern "C" int pkt_probe_stream_copy(const uint8_t* const* srcs, uint8_t* const* dsts, uint32_t k, uint64_t read_bytes,
+                                     uint64_t write_bytes, void* stream) {
+    if (!srcs || !dsts || k == 0 || k > (uint32_t)kCopyMax || (read_bytes & 15) || (write_bytes & 15) ||
+        (read_bytes == 0 && write_bytes == 0))
+        return PKT_ERR_INVALID_ARG;
+    CopyArgs a;
+    for (uint32_t b = 0; b < (uint32_t)kCopyMax; b++) {
+        const uint32_t q = b < k ? b : 0;
+        if (((uintptr_t)srcs[q] & 15) || ((uintptr_t)dsts[q] & 15) || !srcs[q] || !dsts[q]) return PKT_ERR_INVALID_ARG;
+        a.src[b] = reinterpret_cast<const uint4*>(srcs[q]);
+        a.dst[b] = reinterpret_cast<uint4*>(dsts[q]);
+    }
+    a.nr = read_bytes / 16;
+    a.nw = write_bytes / 16;
+    const uint64_t nc = a.nr > a.nw ? a.nr : a.nw;
+    const uint64_t bpb = (nc + 256u * kCopyU - 1) / (256u * kCopyU);
+    if (bpb * k >= (1ull << 31)) return PKT_ERR_INVALID_ARG;
+    a.bpb = (uint32_t)bpb;
+    hipLaunchKernelGGL(stream_copy_kernel, dim3((unsigned)(bpb * k)), dim3(256), 0, reinterpret_cast<hipStream_t>(stream), a);
+    return hipGetLastError() == hipSuccess ? PKT_SUCCESS : PKT_ERR_HIP;
+}

@@ -975,7 +975,13 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
         if (!ctx->tv_flag &&
             (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), pkt_ctx::kTvFlags * sizeof(uint32_t))) != hipSuccess)
             return hip_fail(ctx, e, "hipMalloc (to_vec flag)");
-        uint32_t* flag = ctx->tv_flag + (ctx->tv_next++ % pkt_ctx::kTvFlags);
+        const uint32_t slot = ctx->tv_next++ % pkt_ctx::kTvFlags;
+        uint32_t* flag = ctx->tv_flag + slot;
+        hipEvent_t& ev = ctx->tv_ev[slot];
+        if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(ctx, e, "hipEventCreate (to_vec flag)");
+        // the word's previous user (a call 256 calls ago, maybe on another stream) has read it
+        if ((e = hipStreamWaitEvent(s, ev, 0)) != hipSuccess) return hip_fail(ctx, e, "hipStreamWaitEvent");
         if ((e = hipMemsetAsync(flag, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
         hipLaunchKernelGGL(tv_overlap_kernel, dim3((unsigned)((b->n - 1 + 255) / 256)), dim3(256), 0, s, b->offsets,
                            b->lens, b->n, flag);
@@ -984,6 +990,8 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
     }
     hipLaunchKernelGGL(to_vec_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), tp);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");
+    if (tp.overlap && (e = hipEventRecord(ctx->tv_ev[(ctx->tv_next - 1) % pkt_ctx::kTvFlags], s)) != hipSuccess)
+        return hip_fail(ctx, e, "hipEventRecord (to_vec flag)");
     return PKT_SUCCESS;
 }
 

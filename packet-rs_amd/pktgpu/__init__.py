@@ -444,6 +444,16 @@ class Parser:
         k = min(cap, n.value)
         return offs[:k], lens[:k], n.value
 
+    def pcap_index_device_timed(self, buf, offsets, lens, stream=None):
+        """pkt_pcap_index_device_timed into the caller's device `offsets` / `lens` (cap = their
+        length): (record count, [guess, scan, emit] kernel ms from HIP events between them)."""
+        n = ctypes.c_uint64()
+        ms = (ctypes.c_float * 3)()
+        self._check(self._L.pkt_pcap_index_device_timed(self._ctx, buf.data_ptr(), buf.numel(), offsets.data_ptr(),
+                                                        lens.data_ptr(), offsets.numel(), ctypes.byref(n),
+                                                        self._stream(stream), ms), "pkt_pcap_index_device_timed")
+        return n.value, [ms[0], ms[1], ms[2]]
+
 
 def pcap_index(buf):
     """(offsets uint64, lens uint32) of a tests/pcap.rs-format buffer, via the C ABI."""

@@ -104,6 +104,9 @@ SIGNATURES = {
                                       ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_pcap_index_device": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
                                              ctypes.POINTER(ctypes.c_uint64), _P]),
+    "pkt_pcap_index_device_timed": (ctypes.c_int, [_P, _P, ctypes.c_uint64, _P, _P, ctypes.c_uint64,
+                                                   ctypes.POINTER(ctypes.c_uint64), _P,
+                                                   ctypes.POINTER(ctypes.c_float)]),
     "pkt_parse_pcap": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut), _P, _P,
                                       ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64), _P]),
     "pkt_parse_pcap_host_async": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int, ctypes.POINTER(PktOut),
@@ -131,6 +134,7 @@ SIGNATURES = {
                                        ctypes.POINTER(PktGatherPiece), ctypes.c_uint64,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_mgpu_set_root_copy": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pkt_mgpu_set_gather_rows": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_mgpu_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),

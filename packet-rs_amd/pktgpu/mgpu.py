@@ -139,6 +139,11 @@ class MultiParser:
         send/recv to itself (False)."""
         self._check(self._L.pkt_mgpu_set_root_copy(self._mg, int(bool(enable))), "pkt_mgpu_set_root_copy")
 
+    def set_gather_rows(self, rows):
+        """pkt_mgpu_set_gather_rows: slot rows parse_gather moves per shard (0 = each shard's largest
+        n_hdrs, measured in its parse: the host waits for it; 1..16 = fixed, no host wait)."""
+        self._check(self._L.pkt_mgpu_set_gather_rows(self._mg, int(rows)), "pkt_mgpu_set_gather_rows")
+
     def synchronize(self):
         self._check(self._L.pkt_mgpu_synchronize(self._mg), "pkt_mgpu_synchronize")
 

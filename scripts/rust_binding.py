@@ -14,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(REPO, "include", "pktgpu.h")
 
 C_SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64", "int32_t": "i32",
-             "int": "c_int", "size_t": "usize", "char": "c_char", "void": "c_void",
+             "int": "c_int", "float": "f32", "size_t": "usize", "char": "c_char", "void": "c_void",
              "pkt_ctx_t": "PktCtx", "pkt_batch_t": "PktBatch", "pkt_out_t": "PktOut", "pkt_chain_t": "PktChain",
              "pkt_field_spec_t": "PktFieldSpec", "pkt_gen_field_t": "PktGenField", "pkt_gen_t": "PktGen",
              "pkt_mgpu_t": "PktMgpu", "pkt_gather_piece_t": "PktGatherPiece"}

@@ -790,3 +790,31 @@ def test_parse_batches_vs_oracle(P, same):
     P.parse_batches(bts, outs)
     for k in range(3):
         compare({c: v.cpu().numpy() for c, v in outs[k].items()}, refs[k], f"c4 batch {k}")
+
+
+def test_parse_batches_ipv6_alignment(P):
+    """pkt_parse_batches' one-launch path addresses batch k's columns as batch 0's + a
+    common distance, so it is taken only when that distance keeps the IPv6 address columns 16-byte
+    aligned.  Distance % 16 == 0 (but not a multiple of 256): one launch, every batch == oracle;
+    distance % 16 == 8: the per-batch path validates each batch and rejects the misaligned one."""
+    import torch
+    from pktgpu.mgpu import packed_bytes, packed_views
+    n = 4096
+    ins, refs = [], []
+    for k in range(2):
+        buf, offs, lens = gen.gen_c4(n, seed=320 + k)
+        ins.append((torch.from_numpy(buf).cuda(), n, None, torch.from_numpy(offs).cuda(),
+                    torch.from_numpy(lens).cuda()))
+        refs.append(oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8))
+    nb = (packed_bytes("all", n) + 255) // 256 * 256
+    for pad, ok in ((16, True), (8, False)):
+        dist = nb + pad
+        big = torch.full((2 * dist + 256,), 0xEE, dtype=torch.uint8, device="cuda")
+        outs = [packed_views(big[k * dist:], "all", n) for k in range(2)]
+        if ok:
+            P.parse_batches(ins, outs)
+            for k in range(2):
+                compare({c: v.cpu().numpy() for c, v in outs[k].items()}, refs[k], f"pad {pad} batch {k}")
+        else:
+            with pytest.raises(RuntimeError):
+                P.parse_batches(ins, outs)

@@ -394,3 +394,35 @@ def test_mgpu_parse_steps_vs_oracle(MP, streams):
                 continue
             got = {c: v.cpu().numpy() for c, v in packed_views(steps[k][i][1], cols, n).items()}
             _compare(got, oracle.parse_batch(slab, n, stride=64, columns=cols, nthreads=8), f"step {k} dev {i}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("root_copy", [True, False])
+def test_mgpu_parse_gather_fixed_rows_and_repack(MP, root_copy):
+    """pkt_mgpu_set_gather_rows(k) queues parse + gather with no host wait (k slot rows
+    per shard, >= every n_hdrs), and merge = 1 is the merge = 0 transfer into the root's staging area
+    plus the repack kernel (root copy on: the root's own pieces repacked straight from its shard
+    buffer; off: through RCCL and the staging area).  Odd batch sizes put the slot rows at offsets that
+    are not 16-byte aligned (the repack's head / tail bytes).  Every mode == oracle."""
+    n = 40_001
+    buf, offs, lens = gen.gen_c4(n, seed=81)
+    cols = list(schema.COLUMN_NAMES)
+    shards = MP.shard_indexed(buf, offs, lens)
+    o = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    rows_needed = int(o["n_hdrs"].max())
+    MP.set_root_copy(root_copy)
+    try:
+        for rows in (16, rows_needed, 0):
+            MP.set_gather_rows(rows)
+            for merge in (True, False):
+                views, recv, _ = MP.parse_gather(shards, columns=cols, merge=merge)
+                MP.synchronize()
+                if merge:
+                    _compare(views, o, f"rows {rows} merged root_copy={root_copy}")
+                else:
+                    merged = {c: np.concatenate([v[c].cpu().numpy() for v in views if v],
+                                                axis=1 if c in ("hdr_type", "hdr_off") else 0) for c in cols}
+                    _compare(merged, o, f"rows {rows} per-shard root_copy={root_copy}")
+    finally:
+        MP.set_gather_rows(0)
+        MP.set_root_copy(True)

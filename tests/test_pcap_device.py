@@ -267,3 +267,32 @@ def test_parse_pcap_fused_vs_oracle(P):
         with pytest.raises(RuntimeError):
             P.parse_pcap(dev(bad), 8, out=res)
         assert (res["status"].cpu().numpy() == 0xEE).all()  # an error parses nothing
+
+
+def test_parse_pcap_span_staging_cap_past_count(P):
+    """pkt_parse_pcap with wave-span staging (pkt_ctx_set_staging 2, parse_span_kernel) and
+    cap > count — the span kernel takes the device-produced count: the records up to it equal the
+    oracle, and no column (slot rows included) is written past it; whole waves past the count exit."""
+    import torch
+    n = 50000 + 37  # a partial last wave, then 12 whole waves past the count
+    buf, offs, lens = gen.gen_c4(n, seed=73)
+    cap = n + 777
+    res = P.alloc(cap, "all")
+    for v in res.values():
+        v.view(torch.uint8).fill_(0xEE)
+    P.set_staging(2)
+    try:
+        m, g, o, l = P.parse_pcap(dev(buf), cap, out=res)
+    finally:
+        P.set_staging(0)
+    assert m == n
+    ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+    for k, ov in ref.items():
+        gv = g[k].cpu().numpy()
+        if k in ("hdr_type", "hdr_off"):
+            valid = np.arange(schema.MAX_HDRS)[:, None] < ref["n_hdrs"].astype(np.int64)[None, :]
+            assert not (valid & (gv[:, :n] != ov)).any(), k
+            assert (gv[:, n:].view(np.uint8) == 0xEE).all(), k
+        else:
+            assert np.array_equal(gv[:n], ov), k
+            assert (gv[n:].view(np.uint8) == 0xEE).all(), k
