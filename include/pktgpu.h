@@ -270,6 +270,10 @@ int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
  * states).  Results are identical in every mode. */
 int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
 
+/* Tuning knob: bytes of file per copied piece of pkt_parse_pcap_host (pinned columns): 0 = the
+ * default (16 MiB), else any value >= 4096.  Results are identical for every value. */
+int         pkt_ctx_set_host_piece(pkt_ctx_t *ctx, uint64_t bytes);
+
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
  * Asynchronous on `stream`; returns after the launch.  `batch` and `out` may also point into pinned
@@ -303,13 +307,19 @@ int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pk
                    uint64_t chunk);
 /* The capture path of tests/pcap.rs:7-37 end to end, host memory in and out: a pcap file in HOST
  * memory (`buf`, `len` bytes; pinned from pkt_host_alloc for the full link rate) is copied to the
- * device once, indexed there (pkt_pcap_index_device: same records, count, cap behaviour and errors
+ * device, indexed there (pkt_pcap_index_device: same records, count, cap behaviour and errors
  * as pkt_pcap_index) and parsed with `entry` (an indexed batch over the file in place); the requested
  * columns of `out` are HOST memory sized for `cap` records, slot columns strided by cap
  * ([PKT_MAX_HDRS][cap]).  Pinned columns are written by the parse kernel over the link directly; others
  * through the staged pipeline of pkt_parse_host.  offsets / lens (HOST, [cap], may be NULL) receive
  * the records' (data offset, incl_len).  *n_out = the record count (> cap: only the first cap are
- * parsed).  Blocking.  One host call at a time per ctx. */
+ * parsed).  Blocking.  One host call at a time per ctx.
+ * With pinned columns and a file longer than one piece (pkt_ctx_set_host_piece) the file is copied in
+ * pieces and parsed while it arrives: once piece k has landed, the prefix [0, end of piece k) is
+ * indexed (a record running past a prefix's end belongs to a later prefix) and the records it adds to
+ * the previous prefix's are parsed, their columns flowing out over the link while piece k + 1 flows
+ * in.  The last prefix is the whole file, indexed with pkt_pcap_index's errors; on such an error the
+ * records of the earlier prefixes may already be written to `out`. */
 int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                         uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out);
 /* pkt_parse_pcap_host without the wait, for a stream of captures (cap <= 2^26, every column of `out`

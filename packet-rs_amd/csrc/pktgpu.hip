@@ -350,11 +350,12 @@ __host__ __device__ constexpr int waves_per_eu(int nch, int wk) {
 template <int NCH, uint32_t GM, int WK, int LATE = L_EARLY>
 __device__ __forceinline__ void parse_block(const KParams& p, uint32_t blk, uint8_t* lds, const DispatchLds* T,
                                             uint64_t* pkt_st, uint32_t mb = 0) {
-    const uint32_t base = blk * (uint32_t)kBlock;  // within this launch
+    uint32_t base = blk * (uint32_t)kBlock;  // within this launch
     uint32_t n_eff = p.n;
     if (p.n_dev) {  // wave-uniform: the count the device produced (scalar load)
         const uint64_t nd = *p.n_dev;
         n_eff = nd < (uint64_t)n_eff ? (uint32_t)nd : n_eff;
+        if (p.i0_dev) base += (uint32_t)*p.i0_dev;  // the launch starts at a device-produced index
         if (base >= n_eff) return;  // the whole block is past the count
     }
     const bool act = base + threadIdx.x < n_eff;
@@ -606,14 +607,15 @@ template <int NCH, uint32_t GM, int WK>
 __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
     extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
     const uint32_t lane = threadIdx.x;
-    uint32_t n_eff = p.n;
+    uint32_t n_eff = p.n, b0 = blockIdx.x * kSpanBlock;
     if (p.n_dev) {  // wave-uniform: the count the device produced (scalar load)
         const uint64_t nd = *p.n_dev;
         n_eff = nd < (uint64_t)n_eff ? (uint32_t)nd : n_eff;
-        if (blockIdx.x * kSpanBlock >= n_eff) return;  // the whole wave (= block) is past the count
+        if (p.i0_dev) b0 += (uint32_t)*p.i0_dev;  // the launch starts at a device-produced index
+        if (b0 >= n_eff) return;  // the whole wave (= block) is past the count
     }
     const DispatchLds* T = tables<WK>(lds, span_region(NCH), lane, kSpanBlock);
-    const uint32_t i = blockIdx.x * kSpanBlock + lane;  // within this launch
+    const uint32_t i = b0 + lane;  // within this launch
     const bool active = i < n_eff;
     uint64_t off = 0;
     uint32_t len = 0;
@@ -685,18 +687,18 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
 enum LaunchMode { M_TILE = 0, M_SPAN = 2 };
 
 template <int NCH, uint32_t GM, int WK>
-hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiParams* mp) {
+hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiParams* mp, uint32_t gn) {
     if (mp) {  // several batches, one launch (windows only)
         hipLaunchKernelGGL((parse_multi_kernel<NCH, GM, WK>), dim3(mp->bpb * mp->k), dim3(kBlock),
                            with_tables(window_lds(NCH), WK), s, *mp);
         return hipGetLastError();
     }
     if (mode == M_SPAN) {
-        hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kSpanBlock - 1) / kSpanBlock)),
+        hipLaunchKernelGGL((parse_span_kernel<NCH, GM, WK>), dim3((unsigned)((gn + kSpanBlock - 1) / kSpanBlock)),
                            dim3(kSpanBlock), with_tables(span_region(NCH), WK), s, kp);
     } else {
         const size_t lds = with_tables(window_lds(NCH), WK);
-        hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((kp.n + kBlock - 1) / kBlock)), dim3(kBlock),
+        hipLaunchKernelGGL((parse_kernel<NCH, GM, WK>), dim3((unsigned)((gn + kBlock - 1) / kBlock)), dim3(kBlock),
                            lds, s, kp);
     }
     return hipGetLastError();
@@ -705,23 +707,24 @@ hipError_t launch_mode(const KParams& kp, int mode, hipStream_t s, const MultiPa
 // Kernels are compiled per fully-requested column-group set; the lockstep walk (mixed traffic)
 // only for the chain-only, all-columns and per-column-check sets.
 template <int NCH>
-hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s, const MultiParams* mp) {
+hipError_t launch_gm(const KParams& kp, uint32_t gm, int mode, int wk, hipStream_t s, const MultiParams* mp,
+                     uint32_t gn) {
     // lockstep (indexed batches; non-temporal column stores): compiled for the windows of 6, 7, 9
     // and 17 chunks only (window requests of <= 80, 96, 128 and 256 B; parse_impl widens the rest)
     if constexpr (NCH >= 6) if (wk == 1) {
         switch (gm) {
-            case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp);
-            case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp);
-            default: return launch_mode<NCH, G_RUNTIME | G_NT, 1>(kp, mode, s, mp);
+            case G_CHAIN: return launch_mode<NCH, G_CHAIN | G_NT, 1>(kp, mode, s, mp, gn);
+            case G_ALL: return launch_mode<NCH, G_ALL | G_NT, 1>(kp, mode, s, mp, gn);
+            default: return launch_mode<NCH, G_RUNTIME | G_NT, 1>(kp, mode, s, mp, gn);
         }
     }
     switch (gm) {
-        case G_CHAIN: return launch_mode<NCH, G_CHAIN, 0>(kp, mode, s, mp);
-        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP, 0>(kp, mode, s, mp);
+        case G_CHAIN: return launch_mode<NCH, G_CHAIN, 0>(kp, mode, s, mp, gn);
+        case G_CHAIN | G_ETHER | G_IPV4 | G_UDP: return launch_mode<NCH, G_CHAIN | G_ETHER | G_IPV4 | G_UDP, 0>(kp, mode, s, mp, gn);
         case G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP:
-            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP, 0>(kp, mode, s, mp);
-        case G_ALL: return launch_mode<NCH, G_ALL, 0>(kp, mode, s, mp);
-        default: return launch_mode<NCH, G_RUNTIME, 0>(kp, mode, s, mp);
+            return launch_mode<NCH, G_CHAIN | G_ETHER | G_VLAN | G_IPV4 | G_TCP | G_UDP, 0>(kp, mode, s, mp, gn);
+        case G_ALL: return launch_mode<NCH, G_ALL, 0>(kp, mode, s, mp, gn);
+        default: return launch_mode<NCH, G_RUNTIME, 0>(kp, mode, s, mp, gn);
     }
 }
 
@@ -911,6 +914,9 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         (void)hipFree(ctx->hp.file);
         (void)hipFree(ctx->hp.ioffs);
         (void)hipFree(ctx->hp.ilens);
+        (void)hipFree(ctx->hp.pcnt);
+        for (uint32_t k = 0; k < ctx->hp.pev_n; k++) (void)hipEventDestroy(ctx->hp.pev[k]);
+        delete[] ctx->hp.pev;
     }
     delete ctx;
     return PKT_SUCCESS;
@@ -942,9 +948,16 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
     return PKT_SUCCESS;
 }
 
+int pkt_ctx_set_host_piece(pkt_ctx_t* ctx, uint64_t bytes) {
+    if (!ctx || (bytes != 0 && bytes < 4096)) return PKT_ERR_INVALID_ARG;
+    ctx->host_piece = bytes;
+    return PKT_SUCCESS;
+}
+
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                       void* stream, uint64_t off_bias, int staging, uint32_t* nh_max = nullptr,
-                      uint64_t slot_stride = 0, MultiParams* mp = nullptr, const uint64_t* n_dev = nullptr);
+                      uint64_t slot_stride = 0, MultiParams* mp = nullptr, const uint64_t* n_dev = nullptr,
+                      const uint64_t* i0_dev = nullptr, uint64_t grid_n = 0);
 
 int pkt_parse_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                     void* stream) {
@@ -1032,9 +1045,11 @@ int pktgpu_parse_rows_async(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, con
 extern "C" {
 
 // `staging` = the ctx's knob, or the host path's override (wave spans over the link).
+// i0_dev / grid_n (with n_dev, one launch): the launch parses packets [*i0_dev (or 0), min(b->n, *n_dev))
+// with a grid for grid_n packets (the most the device-produced range can hold; 0 = b->n).
 static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out,
                       void* stream, uint64_t off_bias, int staging, uint32_t* nh_max, uint64_t slot_stride,
-                      MultiParams* mp, const uint64_t* n_dev) {
+                      MultiParams* mp, const uint64_t* n_dev, const uint64_t* i0_dev, uint64_t grid_n) {
     if (!ctx || !b || !out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     if (entry < 0 || entry >= PKT_ENTRY_COUNT) return fail(ctx, PKT_ERR_INVALID_ARG, "bad entry");
     if (b->n == 0) return PKT_SUCCESS;
@@ -1093,21 +1108,24 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         kp.fast = ctx->fast && (entry == PKT_ENTRY_PARSE || entry == PKT_ENTRY_ETHERNET);
         kp.nh_max = nh_max;
         kp.n_dev = n_dev;  // (one launch: n_dev is only passed for batches of n <= kLaunchChunk)
+        kp.i0_dev = n_dev ? i0_dev : nullptr;
         pkt_out_t o = *out;
         uint8_t** oc = reinterpret_cast<uint8_t**>(&o);
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
         if (mp) mp->base = kp;  // batch 0 of a multi-batch launch (n <= kLaunchChunk: one chunk)
+        // the launch's grid: kp.n packets, or grid_n when the range starts at a device-produced index
+        const uint32_t gn = (kp.n_dev && grid_n) ? (uint32_t)std::min<uint64_t>(grid_n, cnt) : kp.n;
         const int md = mp ? M_TILE : mode;
         // compiled window widths (chunks): a request between two is served by the wider one
-        if (nch <= 2) e = launch_gm<2>(kp, gm, md, wk, s, mp);
-        else if (nch <= 4) e = launch_gm<4>(kp, gm, md, wk, s, mp);
-        else if (nch <= 5) e = launch_gm<5>(kp, gm, md, wk, s, mp);
-        else if (nch <= 6) e = launch_gm<6>(kp, gm, md, wk, s, mp);
-        else if (nch <= 7 && wk == 1) e = launch_gm<7>(kp, gm, md, wk, s, mp);
-        else if (nch <= 9) e = launch_gm<9>(kp, gm, md, wk, s, mp);
-        else e = launch_gm<17>(kp, gm, md, wk, s, mp);
+        if (nch <= 2) e = launch_gm<2>(kp, gm, md, wk, s, mp, gn);
+        else if (nch <= 4) e = launch_gm<4>(kp, gm, md, wk, s, mp, gn);
+        else if (nch <= 5) e = launch_gm<5>(kp, gm, md, wk, s, mp, gn);
+        else if (nch <= 6) e = launch_gm<6>(kp, gm, md, wk, s, mp, gn);
+        else if (nch <= 7 && wk == 1) e = launch_gm<7>(kp, gm, md, wk, s, mp, gn);
+        else if (nch <= 9) e = launch_gm<9>(kp, gm, md, wk, s, mp, gn);
+        else e = launch_gm<17>(kp, gm, md, wk, s, mp, gn);
     }
     if (e != hipSuccess) return hip_fail(ctx, e, "parse_kernel launch");
     return PKT_SUCCESS;
@@ -1419,6 +1437,86 @@ int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
     return pktgpu_pcap_take(ctx, n_out);
 }
 
+}  // extern "C"
+
+constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
+
+// pkt_parse_pcap_host with pinned columns, piece by piece (include/pktgpu.h): piece k's copy on hp.s[1];
+// on hp.s[0], once it has landed, the index of the prefix [0, hi_k) (partial: a record running past hi_k
+// is left to a later prefix; the last prefix is the file, with the errors) writing its record count to
+// count word k, and the parse of records [count k-1, count k) writing the pinned columns over the link
+// while the next pieces copy in.  The records a prefix adds all end in (hi_{k-1}, hi_k] and are disjoint
+// (>= 16 B each), so at most (hi_k - hi_{k-1}) / 16 + 1 of them: that sizes each parse's grid.
+static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t& dout,
+                            uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out, uint64_t piece) {
+    HostPipe& hp = ctx->hp;
+    hipStream_t cs = hp.s[1], ps = hp.s[0];
+    const uint64_t np64 = (len + piece - 1) / piece;
+    if (np64 > (1u << 20)) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host: too many pieces");
+    const uint32_t np = (uint32_t)np64;
+    hipError_t e = hipSuccess;
+    if (np > hp.pcnt_cap) {
+        (void)hipFree(hp.pcnt);
+        hp.pcnt = nullptr;
+        hp.pcnt_cap = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&hp.pcnt), (uint64_t)np * 8)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMalloc (piece counts)");
+        hp.pcnt_cap = np;
+    }
+    if (np > hp.pev_n) {
+        hipEvent_t* ev = new hipEvent_t[np]();
+        for (uint32_t k = 0; k < hp.pev_n; k++) ev[k] = hp.pev[k];
+        delete[] hp.pev;
+        hp.pev = ev;
+        for (uint32_t k = hp.pev_n; k < np && e == hipSuccess; k++) {
+            e = hipEventCreateWithFlags(&hp.pev[k], hipEventDisableTiming);
+            if (e == hipSuccess) hp.pev_n = k + 1;
+        }
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate (pieces)");
+    }
+    int rc = pktgpu_pcap_reserve(ctx, len, ps);  // the whole file's scratch: no growth between prefixes
+    if (rc != PKT_SUCCESS) return rc;
+    auto bail = [&](int code) {  // nothing left in flight that reads `buf` or writes `out`
+        (void)hipStreamSynchronize(cs);
+        (void)hipStreamSynchronize(ps);
+        return code;
+    };
+    uint64_t hi_prev = 0;
+    for (uint32_t k = 0; k < np; k++) {
+        const uint64_t lo = (uint64_t)k * piece, hi = std::min(len, lo + piece);
+        if ((e = hipMemcpyAsync(hp.file + lo, buf + lo, hi - lo, hipMemcpyHostToDevice, cs)) != hipSuccess ||
+            (e = hipEventRecord(hp.pev[k], cs)) != hipSuccess || (e = hipStreamWaitEvent(ps, hp.pev[k], 0)) != hipSuccess)
+            return bail(hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap piece)"));
+        const bool last = k + 1 == np;
+        const uint64_t* cnt = nullptr;
+        if ((rc = pktgpu_pcap_launch(ctx, hp.file, hi, hp.ioffs, hp.ilens, cap, ps, &cnt, !last, hp.pcnt + k)) != PKT_SUCCESS)
+            return bail(rc);
+        pkt_batch_t db;
+        db.slab = hp.file;
+        db.slab_len = hi;  // the prefix: every record parsed here lies inside it
+        db.offsets = hp.ioffs;
+        db.lens = hp.ilens;
+        db.stride = 0;
+        db.reserved = 0;
+        db.n = cap;
+        rc = parse_impl(ctx, &db, entry, &dout, ps, 0, ctx->staging, nullptr, cap, nullptr, cnt,
+                        k ? hp.pcnt + (k - 1) : nullptr, (hi - hi_prev) / 16 + 1);
+        if (rc != PKT_SUCCESS) return bail(rc);
+        hi_prev = hi;
+    }
+    if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
+    if ((rc = pktgpu_pcap_finish(ctx, n_out)) != PKT_SUCCESS) return rc;
+    const uint64_t m = std::min(*n_out, cap);
+    if (m && offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, ps)) != hipSuccess)
+        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)"));
+    if (m && lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, ps)) != hipSuccess)
+        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)"));
+    if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
+    return PKT_SUCCESS;
+}
+
+extern "C" {
+
 int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
                         uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out) {
     if (!ctx || !buf || !out || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
@@ -1429,6 +1527,12 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
     hipStream_t s = hp.s[0];
+    {  // pinned columns and more than one piece: copy, index and parse piece by piece
+        pkt_out_t dout;
+        const uint64_t piece = ctx->host_piece ? ctx->host_piece : kHostPiece;
+        if (len > piece && cap && cap <= kLaunchChunk && out_mapped(out, dout))
+            return pcap_host_pieces(ctx, buf, len, entry, dout, offsets, lens, cap, n_out, piece);
+    }
     // every error return after the first queued copy waits for the ctx's streams first: a copy from
     // `buf` or into `offsets` / `lens` must not outlive the call
     auto bail = [&](int code) {

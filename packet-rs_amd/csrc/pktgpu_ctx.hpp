@@ -24,6 +24,12 @@ struct HostPipe {
     uint64_t* ioffs = nullptr;
     uint32_t* ilens = nullptr;
     uint64_t file_cap = 0, idx_cap = 0;  // bytes; records
+    // the piecewise capture: one device count word per piece (the records of the file's prefix up to
+    // the piece's end), one copy-done event per piece
+    uint64_t* pcnt = nullptr;
+    uint32_t pcnt_cap = 0;
+    hipEvent_t* pev = nullptr;
+    uint32_t pev_n = 0;
 };
 
 // Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.
@@ -84,6 +90,7 @@ struct pkt_ctx {
     int fast;         // register fast path for Ether/IPv4/UDP|TCP packets
     int staging;      // 0 = auto, 1 = per-lane windows, 2 = wave span (LDS-DMA)
     int walk;         // 0 = auto, 1 = waterfall, 2 = lockstep
+    uint64_t host_piece = 0;  // pkt_parse_pcap_host: bytes of file per copied piece (0 = kHostPiece)
     // pkt_to_vec_batch: device words, nonzero = a chunk holds bytes of two records; a ring, one word
     // per call, so calls in flight on several streams do not share one; a word is reused only after
     // the call that last used it has passed its to_vec kernel (the call's stream waits on tv_ev[k])
@@ -120,8 +127,13 @@ int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const 
 // The device pcap indexer's kernels queued on `stream` (no host wait; *count_dev = the device word
 // holding the record count, 0 after an error), and its outcome once the stream has passed them
 // (pktgpu_pcap.hip).  Used by pkt_parse_pcap_host_async (pktgpu.hip).
+// partial / count_out: index buf[0, len) as the PREFIX of a capture still arriving (a record running past
+// its end ends the index, no error) and write the record count to the device word count_out (NULL: the
+// ctx's own word, returned in *count_dev either way).  pktgpu_pcap_reserve: scratch for a file of len bytes.
 int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                       uint64_t cap, hipStream_t s, const uint64_t** count_dev);
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, bool partial = false,
+                       uint64_t* count_out = nullptr);
+int pktgpu_pcap_reserve(pkt_ctx_t* ctx, uint64_t len, hipStream_t s);
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out);
 int pktgpu_pcap_take(pkt_ctx_t* ctx, uint64_t* n_out);  // a queued capture's outcome (waits; clears pending)
 

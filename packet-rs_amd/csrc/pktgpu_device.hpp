@@ -59,6 +59,9 @@ struct KParams {
     pkt_out_t out;
     const uint64_t* n_dev;  // non-NULL: the batch holds min(n, *n_dev) packets (a count produced on the
                             // device, e.g. by the pcap indexer; blocks past it exit)
+    const uint64_t* i0_dev;  // non-NULL (with n_dev): this launch parses packets [*i0_dev, min(n, *n_dev)) —
+                             // block b takes packets *i0_dev + 256 b ... (pkt_parse_pcap_host's pieces: the
+                             // records a prefix index added to the one before)
     uint32_t* nh_max;  // non-NULL: the batch's largest n_hdrs (the used slot rows), spread over kMaxSpread
                        // words (wave maxima atomicMax'ed into word blockIdx % kMaxSpread; the host
                        // takes the max of the words)
@@ -386,6 +389,10 @@ constexpr uint32_t kDwHi[10]       = {0,   0,  8,  0,  0,   0,  2,  0,    0, 0};
 constexpr uint64_t kSz0 = pack6(kSzLo, 0), kSz1 = pack6(kSzHi, 10);
 constexpr uint64_t kTy0 = pack6(kTyLo, 0), kTy1 = pack6(kTyHi, 10);
 constexpr uint64_t kDw0 = pack6(kDwLo, 0), kDw1 = pack6(kDwHi, 10);
+// states whose next state (or option / platform test) depends on their dispatch dword D (lstep)
+constexpr uint32_t kNeedsD = (1u << S_PARSE) | (1u << S_LLC) | (1u << S_ETHER) | (1u << S_VLAN) | (1u << S_MPLS) |
+                             (1u << S_MPLS_BOS) | (1u << S_IPV4) | (1u << S_IPV6) | (1u << S_GRE) |
+                             (1u << S_ERSPAN3) | (1u << S_UDP);
 
 __device__ __forceinline__ uint32_t tab6(uint64_t lo, uint64_t hi, uint32_t st) {
     const bool h = st >= 10u;
@@ -546,7 +553,10 @@ __device__ __forceinline__ void walk(PacketView& pv, uint32_t state, bool active
             const bool in_win = b >= pv.win_lo && b + 4 <= pv.win_end;
             const uint32_t wb = in_win ? b + pv.shift : 0u, k = wb >> 2, sh = wb & 3;
             uint32_t D = __builtin_amdgcn_alignbyte(w[k + 1], w[k], sh);
-            const bool far = live && !in_win && L.st != S_ACCEPT && L.steps < PKT_MAX_HDRS + 3 &&
+            // (only states whose next state depends on D read it from memory: DOT3 -> LLC, SNAP / ARP /
+            // ICMP / TCP -> accept and ERSPAN2 / VXLAN -> Ether whatever their bytes hold, so a lane
+            // in one of them past the window issues no read — C4's inner TCP / ICMP headers)
+            const bool far = live && !in_win && ((kNeedsD >> L.st) & 1u) && L.steps < PKT_MAX_HDRS + 3 &&
                              L.o + tab6(kSz0, kSz1, L.st) <= pv.len;
             if (__ballot(far)) {
                 if (far) D = pv.le(b, 4);

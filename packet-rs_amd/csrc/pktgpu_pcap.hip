@@ -91,7 +91,12 @@ struct Scratch {
     uint64_t* host;    // kHostWords pinned words (device address)
     uint64_t* dev;     // device words: [0] the record count for a parse that follows on the device (0 after
                        // an error), [1] the magic check (guess region 0)
+    uint64_t* count_out;  // where the last scan block writes that count (dev + 0 unless the caller names a word)
     uint32_t epoch;
+    // partial = 1: the buffer is a PREFIX of a capture still arriving (pkt_parse_pcap_host's pieces): a
+    // record running past its end ends the index without an error (the walks' error bit is dropped, so
+    // the record is neither counted nor an error) — the records counted are those wholly inside it
+    uint32_t partial;
 };
 
 // The aggregate of a run of regions:
@@ -510,6 +515,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
                 lane_walk2(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, kk < K, ex, cw);
             else if (kk < K)
                 lane_walk(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, ex, cw);
+            if (S.partial) cw &= kCntMask;
             s_exit[lane] = ex;
             s_cnt[lane] = cw;
         }
@@ -558,6 +564,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     // profiles/ab/r03i_pcap_uniform_walk.txt)
     uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
     walk(lw, lbase, PKTGPU_PCAP_GLIST ? dst : lst[w], base, entry, len, exit, cnt, err, rec);
+    if (S.partial) err = 0;
     wave_lds_sync();
     if (lane < cnt) dst[lane] = (uint16_t)rec;
     if constexpr (!PKTGPU_PCAP_GLIST)
@@ -761,6 +768,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                     lane_walk2(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, true, ex, cw);
                 wave_lds_sync();
                 cw = (uint32_t)__shfl((int)cw, 0, 64);
+                if (S.partial) cw &= kCntMask;
                 ex = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex >> 32), 0, 64) << 32) |
                      (uint32_t)__shfl((int)(uint32_t)ex, 0, 64);
                 const uint32_t cnt = cw & kCntMask;
@@ -779,6 +787,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             uint64_t exit;
             uint32_t cnt, err, rec;
             walk(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, exit, cnt, err, rec);
+            if (S.partial) err = 0;
             wave_lds_sync();
             uint16_t* dst = S.list + (uint64_t)kk * kMaxRec;
             if (lane < cnt) dst[lane] = (uint16_t)rec;
@@ -987,7 +996,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             __hip_atomic_store(&S.host[kHostTotal], c_before + total.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // the count a parse on the same stream reads (kernel boundary: no fence needed); 0 when
             // the call fails (bad magic, a record past the end), so that parse writes nothing
-            S.dev[0] = (S.dev[1] && !err_all) ? c_before + total.cnt : 0;
+            *S.count_out = (S.dev[1] && !err_all) ? c_before + total.cnt : 0;
             __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err_all ? 1 : 0), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
         }
@@ -1073,10 +1082,43 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
 // Queue the index of the pcap file `buf` on `s` (guess + scan kernels; the scan writes the records):
 // no host synchronisation.  *count_dev = the device word a following parse may take its record count
 // from (0 after an error).  pcap_finish reads the outcome once the stream is synchronised.
+// The index scratch for K regions (grown on demand, after `s` has drained).
+static hipError_t pcap_reserve(pkt_ctx_t* ctx, uint32_t K, hipStream_t s) {
+    PcapScratch& pc = ctx->pc;
+    if (K <= pc.k_cap) return hipSuccess;
+    if (pc.buf) {
+        (void)hipStreamSynchronize(s);
+        (void)hipFree(pc.buf);
+        pc.buf = nullptr;
+        pc.bytes = 0;
+        pc.k_cap = pc.nb_cap = 0;
+    }
+    const uint32_t kc = K + K / 4 + 64, nbc = (kc + kScanRegions - 1) / kScanRegions;
+    const uint64_t bytes = 64 + (uint64_t)nbc * sizeof(BlkDesc) + (uint64_t)kc * (8 + 8 + 8 + 4 + 2 * kMaxRec);
+    hipError_t e = hipMalloc(&pc.buf, bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(pc.buf, 0, bytes, s);
+    if (e != hipSuccess) return e;
+    pc.bytes = bytes;
+    pc.k_cap = kc;
+    pc.nb_cap = nbc;
+    return hipSuccess;
+}
+
+int pktgpu_pcap_reserve(pkt_ctx_t* ctx, uint64_t len, hipStream_t s) {
+    const uint64_t K64 = (len + kRegion - 1) / kRegion;
+    if (K64 > (1ull << 31)) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
+    hipError_t e = hipSetDevice(ctx->device);
+    if (e == hipSuccess) e = pcap_reserve(ctx, (uint32_t)K64, s);
+    return e == hipSuccess ? PKT_SUCCESS : hip_fail(ctx, e, "hipMalloc (pcap index)");
+}
+
 // ev (measurement only, pkt_pcap_index_device_timed): 4 events recorded on `s` before the guess
 // kernel and after each of the three kernels.
+// partial / count_out (pkt_parse_pcap_host's pieces): index `buf[0, len)` as the prefix of a capture
+// (Scratch.partial) and leave the record count in the device word count_out instead of the ctx's.
 static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, hipEvent_t* ev = nullptr) {
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, hipEvent_t* ev = nullptr,
+                       bool partial = false, uint64_t* count_out = nullptr) {
     if (!ctx || !buf || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
@@ -1093,23 +1135,7 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // this call's K: the block-state array must never overlay an earlier call's per-region words
     // (file positions and prefixes a look-back could take for a state published in this epoch).
     PcapScratch& pc = ctx->pc;
-    if (K > pc.k_cap) {
-        if (pc.buf) {
-            (void)hipStreamSynchronize(s);
-            (void)hipFree(pc.buf);
-            pc.buf = nullptr;
-            pc.bytes = 0;
-            pc.k_cap = pc.nb_cap = 0;
-        }
-        const uint32_t kc = K + K / 4 + 64, nbc = (kc + kScanRegions - 1) / kScanRegions;
-        const uint64_t bytes = 64 + (uint64_t)nbc * sizeof(BlkDesc) + (uint64_t)kc * (8 + 8 + 8 + 4 + 2 * kMaxRec);
-        e = hipMalloc(&pc.buf, bytes);
-        if (e == hipSuccess) e = hipMemsetAsync(pc.buf, 0, bytes, s);
-        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
-        pc.bytes = bytes;
-        pc.k_cap = kc;
-        pc.nb_cap = nbc;
-    }
+    if ((e = pcap_reserve(ctx, K, s)) != hipSuccess) return hip_fail(ctx, e, "hipMalloc (pcap index)");
     if (!pc.ctl) {
         e = hipHostMalloc(reinterpret_cast<void**>(&pc.ctl), 8 * kHostWords, hipHostMallocMapped);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&pc.ctl_dev), pc.ctl, 0);
@@ -1137,7 +1163,9 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     S.list = reinterpret_cast<uint16_t*>(p);
     S.host = pc.ctl_dev;
     S.dev = reinterpret_cast<uint64_t*>(static_cast<char*>(pc.buf) + 16);
+    S.count_out = count_out ? count_out : S.dev;
     S.epoch = pc.epoch;
+    S.partial = partial ? 1u : 0u;
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
@@ -1165,7 +1193,7 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
-    if (count_dev) *count_dev = S.dev;
+    if (count_dev) *count_dev = S.count_out;
     return PKT_SUCCESS;
 }
 
@@ -1180,8 +1208,8 @@ static int pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) {
 }
 
 int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                       uint64_t cap, hipStream_t s, const uint64_t** count_dev) {
-    return pcap_launch(ctx, buf, len, offsets, lens, cap, s, count_dev);
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, bool partial, uint64_t* count_out) {
+    return pcap_launch(ctx, buf, len, offsets, lens, cap, s, count_dev, nullptr, partial, count_out);
 }
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) { return pcap_finish(ctx, n_out); }
 

@@ -111,6 +111,10 @@ class Parser:
         """0 = auto, 1 = waterfall, 2 = lockstep (pkt_ctx_set_walk)."""
         self._check(self._L.pkt_ctx_set_walk(self._ctx, int(mode)), "pkt_ctx_set_walk")
 
+    def set_host_piece(self, nbytes):
+        """pkt_ctx_set_host_piece: bytes per copied piece of parse_pcap_host (0 = 16 MiB)."""
+        self._check(self._L.pkt_ctx_set_host_piece(self._ctx, int(nbytes)), "pkt_ctx_set_host_piece")
+
     def _check(self, rc, what):
         if rc != 0:
             msg = self._L.pkt_ctx_last_error(self._ctx)

@@ -68,6 +68,7 @@ SIGNATURES = {
     "pkt_ctx_set_fastpath": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_staging": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_walk": (ctypes.c_int, [_P, ctypes.c_int]),
+    "pkt_ctx_set_host_piece": (ctypes.c_int, [_P, ctypes.c_uint64]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
     "pkt_parse_batches": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_uint32, ctypes.c_int,

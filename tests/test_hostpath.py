@@ -219,3 +219,33 @@ def test_pcap_host_async_two_ctx(P):
                                     {"status": np.zeros(len(offs), np.uint8)})
     finally:
         P2.close()
+
+
+@pytest.mark.parametrize("piece", [65537, 1 << 20])
+def test_pcap_host_pieces_vs_oracle(P, piece):
+    """pkt_parse_pcap_host copies a capture in pieces and parses each prefix's new
+    records while the next pieces copy in.  At 2^16 records with pieces of 65537 bytes (odd: the piece
+    boundaries fall inside records and inside record headers) and of 1 MiB, every column, the index
+    and the count equal the host indexer + the oracle; a capture whose last record runs past the end is
+    still an error (the last prefix is the whole file, indexed with pkt_pcap_index's errors)."""
+    n = 1 << 16
+    buf, offs, lens = gen.gen_c4(n, seed=34)
+    cap = n + 77
+    hb = P.host_empty((buf.size,), np.uint8)
+    hb[:] = buf
+    out = {c: P.host_empty(schema.column_shape(c, cap), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
+    P.set_host_piece(piece)
+    try:
+        assert buf.size > 2 * piece
+        m, g, (o2, l2) = P.parse_pcap_host(hb, cap, out=out)
+        assert m == n
+        assert np.array_equal(o2, offs) and np.array_equal(l2, lens)
+        ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+        got = {k: (v[:, :n] if k in ("hdr_type", "hdr_off") else v[:n]) for k, v in g.items()}
+        check(got, ref, f"pcap host pieces of {piece} B")
+        bad = P.host_empty((buf.size - 3,), np.uint8)
+        bad[:] = buf[:-3]  # the last record runs past the end of the file
+        with pytest.raises(RuntimeError):
+            P.parse_pcap_host(bad, cap, out=out)
+    finally:
+        P.set_host_piece(0)
