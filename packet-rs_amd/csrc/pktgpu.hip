@@ -290,6 +290,125 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
+// ---- block-staged column epilogue (build switch PKTGPU_LDS_COLS, the C2 column set) ----
+// The 25 per-packet columns of chain + Ether + IPv4 + UDP are first written into LDS as one run of 256
+// elements per column (the block's packets), then stored by 16-byte chunks: a u8 column's 256 B of a
+// block by 16 consecutive lanes, so a wave instruction writes 256-byte contiguous segments instead of
+// the 64 B (u8) / 128 B (u16) one per-lane narrow store writes (MI355X_MICROARCH: full store rate at
+// 256 contiguous bytes per wave instruction).  The runs are laid out by element size (u64, u32, u16,
+// u8: chunk j's column follows from j by three compares); slot rows stay per-lane stores.
+#ifndef PKTGPU_LDS_COLS
+#define PKTGPU_LDS_COLS 0
+#endif
+constexpr uint32_t kGmC2 = G_CHAIN | G_ETHER | G_IPV4 | G_UDP;
+enum StCol : uint32_t {
+    SC_ETH_DST, SC_ETH_SRC,                                                        // u64
+    SC_MASK, SC_V4SRC, SC_V4DST,                                                   // u32
+    SC_POFF, SC_PLEN, SC_ETYPE, SC_TLEN, SC_IDENT, SC_FRAG, SC_HCSUM, SC_CCALC,    // u16
+    SC_USRC, SC_UDST, SC_ULEN, SC_UCSUM,
+    SC_STATUS, SC_NHDRS, SC_VER, SC_IHL, SC_DIFF, SC_FLAGS, SC_TTL, SC_PROTO,      // u8
+    SC_N
+};
+__host__ __device__ constexpr uint32_t sc_size(uint32_t c) { return c < 2 ? 8u : c < 5 ? 4u : c < 17 ? 2u : 1u; }
+__host__ __device__ constexpr uint32_t sc_off(uint32_t c) {  // LDS byte offset of column c's run
+    return c < 2 ? 2048u * c : c < 5 ? 4096u + 1024u * (c - 2) : c < 17 ? 7168u + 512u * (c - 5) : 13312u + 256u * (c - 17);
+}
+constexpr uint32_t kStageBytes = 15360, kStageChunks = kStageBytes / 16;
+static_assert(sc_off(SC_N - 1) + 256u == kStageBytes && kStageBytes + 8u * SC_N <= 256u * 68u,
+              "the staging runs and the column table fit the C2 windows' LDS");
+__device__ __forceinline__ uint32_t chunk_col(uint32_t j) {
+    return j < 256u ? j >> 7 : j < 448u ? 2u + ((j - 256u) >> 6) : j < 832u ? 5u + ((j - 448u) >> 5) : 17u + ((j - 832u) >> 4);
+}
+__device__ __forceinline__ const void* sc_col(const pkt_out_t& o, uint32_t c) {
+    switch (c) {
+        case SC_ETH_DST: return o.eth_dst;
+        case SC_ETH_SRC: return o.eth_src;
+        case SC_MASK: return o.hdr_mask;
+        case SC_V4SRC: return o.ipv4_src;
+        case SC_V4DST: return o.ipv4_dst;
+        case SC_POFF: return o.payload_off;
+        case SC_PLEN: return o.payload_len;
+        case SC_ETYPE: return o.eth_etype;
+        case SC_TLEN: return o.ipv4_total_len;
+        case SC_IDENT: return o.ipv4_identification;
+        case SC_FRAG: return o.ipv4_frag_startset;
+        case SC_HCSUM: return o.ipv4_header_checksum;
+        case SC_CCALC: return o.ipv4_csum_calc;
+        case SC_USRC: return o.udp_src;
+        case SC_UDST: return o.udp_dst;
+        case SC_ULEN: return o.udp_length;
+        case SC_UCSUM: return o.udp_checksum;
+        case SC_STATUS: return o.status;
+        case SC_NHDRS: return o.n_hdrs;
+        case SC_VER: return o.ipv4_version;
+        case SC_IHL: return o.ipv4_ihl;
+        case SC_DIFF: return o.ipv4_diffserv;
+        case SC_FLAGS: return o.ipv4_flags;
+        case SC_TTL: return o.ipv4_ttl;
+        default: return o.ipv4_protocol;
+    }
+}
+// Thread t of a full 256-packet block: the emit of emit_chain + emit_fields<kGmC2> through the staging
+// runs (lds = the block's window region; every lane must have finished with its window: first barrier).
+template <class View>
+__device__ __forceinline__ void emit_staged_c2(const pkt_out_t& oc, uint32_t base, uint32_t t, uint32_t len,
+                                               const View& pv, const WalkResult& r, uint8_t* lds) {
+    const bool ok = r.status == PKT_OK;
+    uint32_t de[4] = {0, 0, 0, 0}, d4[5] = {0, 0, 0, 0, 0}, du[2] = {0, 0};
+    if (ok && r.f_eth >= 0) pv.template hdr<4>((uint32_t)r.f_eth, 14, de);
+    const bool h4 = ok && r.f_ipv4 >= 0;
+    if (h4) pv.template hdr<5>((uint32_t)r.f_ipv4, 20, d4);
+    if (ok && r.f_udp >= 0) pv.template hdr<2>((uint32_t)r.f_udp, 8, du);
+    __syncthreads();  // every lane has read its window: the region holds the staging runs from here
+    auto w8 = [&](uint32_t c, uint32_t v) { lds[sc_off(c) + t] = (uint8_t)v; };
+    auto w16 = [&](uint32_t c, uint32_t v) { *reinterpret_cast<uint16_t*>(lds + sc_off(c) + 2u * t) = (uint16_t)v; };
+    auto w32 = [&](uint32_t c, uint32_t v) { *reinterpret_cast<uint32_t*>(lds + sc_off(c) + 4u * t) = v; };
+    auto w64 = [&](uint32_t c, uint64_t v) { *reinterpret_cast<uint64_t*>(lds + sc_off(c) + 8u * t) = v; };
+    w8(SC_STATUS, r.status);
+    w8(SC_NHDRS, ok ? r.n : 0u);
+    w16(SC_POFF, ok ? r.payload_off : 0u);
+    w16(SC_PLEN, ok ? len - r.payload_off : 0u);
+    w32(SC_MASK, ok ? r.mask : 0u);
+    w64(SC_ETH_DST, ((uint64_t)de[0] << 16) | (de[1] >> 16));
+    w64(SC_ETH_SRC, ((uint64_t)(de[1] & 0xFFFFu) << 32) | de[2]);
+    w16(SC_ETYPE, de[3] >> 16);
+    w8(SC_VER, d4[0] >> 28);
+    w8(SC_IHL, (d4[0] >> 24) & 0xFu);
+    w8(SC_DIFF, (d4[0] >> 16) & 0xFFu);
+    w16(SC_TLEN, d4[0] & 0xFFFFu);
+    w16(SC_IDENT, d4[1] >> 16);
+    w8(SC_FLAGS, (d4[1] >> 13) & 7u);
+    w16(SC_FRAG, d4[1] & 0x1FFFu);
+    w8(SC_TTL, d4[2] >> 24);
+    w8(SC_PROTO, (d4[2] >> 16) & 0xFFu);
+    w16(SC_HCSUM, d4[2] & 0xFFFFu);
+    w32(SC_V4SRC, d4[3]);
+    w32(SC_V4DST, d4[4]);
+    {  // Packet::ipv4_checksum (packet.rs:93-107), the Q1 fold
+        uint32_t s = (d4[0] >> 16) + (d4[0] & 0xFFFFu) + (d4[1] >> 16) + (d4[1] & 0xFFFFu) + (d4[2] >> 16) +
+                     (d4[3] >> 16) + (d4[3] & 0xFFFFu) + (d4[4] >> 16) + (d4[4] & 0xFFFFu);
+        s = ((s >> 16) + s) & 0xFFFFu;
+        w16(SC_CCALC, h4 ? (~s & 0xFFFFu) : 0u);
+    }
+    w16(SC_USRC, du[0] >> 16);
+    w16(SC_UDST, du[0] & 0xFFFFu);
+    w16(SC_ULEN, du[1] >> 16);
+    w16(SC_UCSUM, du[1] & 0xFFFFu);
+    uint64_t* colp = reinterpret_cast<uint64_t*>(lds + kStageBytes);
+    if (t < SC_N) colp[t] = reinterpret_cast<uint64_t>(sc_col(oc, t)) + (uint64_t)base * sc_size(t);
+    __syncthreads();
+#pragma unroll
+    for (uint32_t k = 0; k < (kStageChunks + kBlock - 1) / kBlock; k++) {
+        const uint32_t j = k * kBlock + t;
+        if (j < kStageChunks) {
+            const uint32_t c = chunk_col(j);
+            const uint4 v = reinterpret_cast<const uint4*>(lds)[j];
+            uint4* g = reinterpret_cast<uint4*>(colp[c] + 16u * (j - (sc_off(c) >> 4)));
+            *as_global(g) = v;
+        }
+    }
+}
+
 // ---- several batches in one launch (pkt_parse_batches) ----
 // K batches of the same size and layout whose outputs lie at one common byte distance from batch
 // 0's (e.g. one packed output buffer each): block j parses tile j % bpb of batch j / bpb.  Every
@@ -524,7 +643,24 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         const uint32_t m = wave_max_u32((active_own && r.status == PKT_OK) ? r.n : 0u);
         if ((t & 63u) == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
-    if (active_own) {
+    bool staged = false;
+    if constexpr (PKTGPU_LDS_COLS && GM == kGmC2 && LATE == L_SINGLE && NCH == 4) {
+        // a full block with aligned columns: every lane emits through the block's staging runs
+        if (p.stage_cols && base + (uint32_t)kBlock <= p.n) {
+            const uint64_t ka = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(KParams, out);
+            uint64_t kav = ka;
+            asm volatile("" : "+s"(kav));
+            const pkt_out_t KARG_AS* kc = reinterpret_cast<const pkt_out_t KARG_AS*>(kav);
+            pkt_out_t oc;
+            const void* const KARG_AS* kp = reinterpret_cast<const void* const KARG_AS*>(kc);
+            void** ocp = reinterpret_cast<void**>(&oc);
+#pragma unroll
+            for (int c = 0; c < 49; c++) ocp[c] = const_cast<void*>(kp[c]);
+            emit_staged_c2(oc, base, t, len_own, pv_own, r, lds);
+            staged = true;
+        }
+    }
+    if (active_own && !staged) {
         if constexpr (LATE != L_EARLY) {
             // The column bases are loaded here, after the walk, by scalar loads from the kernel
             // arguments (an opaque copy of their address keeps the loads from being hoisted to the
@@ -1114,6 +1250,10 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
+        // the block-staged epilogue (PKTGPU_LDS_COLS builds) stores whole 16-byte chunks of each column
+        kp.stage_cols = 1;
+        for (int c = 0; c < 49; c++)
+            if (c != kColHdrType && c != kColHdrOff && oc[c] && ((uintptr_t)oc[c] & 15)) kp.stage_cols = 0;
         if (mp) mp->base = kp;  // batch 0 of a multi-batch launch (n <= kLaunchChunk: one chunk)
         // the launch's grid: kp.n packets, or grid_n when the range starts at a device-produced index
         const uint32_t gn = (kp.n_dev && grid_n) ? (uint32_t)std::min<uint64_t>(grid_n, cnt) : kp.n;

@@ -62,6 +62,8 @@ struct KParams {
     const uint64_t* i0_dev;  // non-NULL (with n_dev): this launch parses packets [*i0_dev, min(n, *n_dev)) —
                              // block b takes packets *i0_dev + 256 b ... (pkt_parse_pcap_host's pieces: the
                              // records a prefix index added to the one before)
+    uint32_t stage_cols;  // PKTGPU_LDS_COLS builds: the C2 column set's bases are 16-byte aligned (the
+                          // block-staged store epilogue may write them by 16-byte chunks)
     uint32_t* nh_max;  // non-NULL: the batch's largest n_hdrs (the used slot rows), spread over kMaxSpread
                        // words (wave maxima atomicMax'ed into word blockIdx % kMaxSpread; the host
                        // takes the max of the words)
@@ -146,6 +148,9 @@ __device__ __forceinline__ void dispatch_init(DispatchLds* T, uint32_t t, uint32
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
+#ifndef PKTGPU_LE_X2
+#define PKTGPU_LE_X2 1  // PacketView::le past the window: one 8-byte load instead of two dword loads
+#endif
 // A lane's view of its packet: LDS window + global fallback.
 struct PacketView {
     const uint8_t* lw;        // LDS window of this packet (dword-aligned)
@@ -179,6 +184,17 @@ struct PacketView {
         }
         const uint64_t a = off + b;
         const uint32_t sh = (uint32_t)(a & 3);
+#if PKTGPU_LE_X2
+        // both dwords by ONE 8-byte load at the 4-byte-aligned address (global_load_dwordx2): two
+        // dword loads are two instructions, and separate instructions to one 128-B line re-request it
+        // from memory
+        const uint64_t d = a & ~(uint64_t)3;
+        if (d + 4 <= last4) {
+            uint32_t v[2];
+            __builtin_memcpy(v, __builtin_assume_aligned(slab + d, 4), 8);
+            return __builtin_amdgcn_alignbyte(v[1], v[0], sh);
+        }
+#endif
         const uint32_t lo = gdw(a);
         const uint32_t hi = (sh + n > 4) ? gdw(a + 4) : 0u;
         return __builtin_amdgcn_alignbyte(hi, lo, sh);

@@ -1037,7 +1037,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
 // thread per step, contiguous in the output (coalesced), at the regions' exact prefix.
 __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
                                                         uint64_t* __restrict__ offsets,
-                                                        uint32_t* __restrict__ lens) {
+                                                        uint32_t* __restrict__ lens, const uint8_t* __restrict__ buf) {
     __shared__ uint32_t cpre[kEmitRegions + 1];
     __shared__ uint64_t cex[kEmitRegions];
     const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
@@ -1072,7 +1072,15 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
         const uint64_t pos = base + list[li];
         const uint64_t next = li + 1 < c ? base + list[li + 1] : cex[r];
         offsets[idx] = pos + 16;
-        lens[idx] = (uint32_t)(next - pos - 16);
+        uint32_t incl = (uint32_t)(next - pos - 16);
+        if (S.partial && li + 1 == c) {
+            // a prefix of a capture: the walk that stopped at a record running past the prefix's end
+            // set its region's exit to that end, not to the record's start — the region's last counted
+            // record takes its incl_len from its own header (bytes pos + 8 .. pos + 11)
+            const uint8_t* h = buf + pos + 8;
+            incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+        }
+        lens[idx] = incl;
     }
 }
 
@@ -1189,7 +1197,7 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
-    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens);
+    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens, buf);
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");

@@ -50,12 +50,14 @@ def chain_ok(b, c, stop, snap, lend=None):
     return 1
 
 
-def walk(b, base, entry):
+def walk(b, base, entry, partial=False):
+    """partial: `b` is a prefix of a capture (pkt_parse_pcap_host's pieces) — a record running past its
+    end stops the walk like an error would, but is no error (the kernels drop the walk's error bit)."""
     pos, lst, err = entry, [], 0
     while pos < base + R and pos + 16 <= len(b):
         incl = u32(b, pos + 8)
         if pos + 16 + incl > len(b):
-            return len(b), lst, 1
+            return len(b), lst, 0 if partial else 1
         lst.append(pos)
         pos += 16 + incl
     return pos, lst, err
@@ -113,7 +115,7 @@ def seam_bad(pre, r):
     return pre[1] < r[1] if r[0] == "none" else pre[1] != r[0]
 
 
-def model_index(b, inject=None, order_seed=None, block=B):
+def model_index(b, inject=None, order_seed=None, block=B, partial=False):
     """The three kernels restated: per-region guesses (`inject` {region: entry} overrides them:
     adversarial wrong guesses) and walks; per scan block of B regions the local fix rounds (a
     region disagreeing with the claiming region before it, while that one agrees with its own
@@ -131,7 +133,7 @@ def model_index(b, inject=None, order_seed=None, block=B):
     st = []
     for k in range(K):  # the guess kernel: every region guesses its own entry
         e = 24 if k == 0 else (inject or {}).get(k, guess(b, k, snap))
-        st.append((e, walk(b, k * R, e)))
+        st.append((e, walk(b, k * R, e, partial)))
     fixed = 0
 
     def local_fixes(lo, hi):
@@ -150,7 +152,7 @@ def model_index(b, inject=None, order_seed=None, block=B):
             if not queue:
                 return pre
             for k, e in queue:  # the waves of one round, from the states the round started with
-                st[k] = (e, walk(b, k * R, e))
+                st[k] = (e, walk(b, k * R, e, partial))
                 fixed += 1
 
     aggs = [local_fixes(q * block, min(K, (q + 1) * block)) for q in range(NB)]
@@ -185,7 +187,7 @@ def model_index(b, inject=None, order_seed=None, block=B):
                 pre = combine(pre, r)
             if todo is None:
                 break
-            st[todo[0]] = (todo[1], walk(b, todo[0] * R, todo[1]))
+            st[todo[0]] = (todo[1], walk(b, todo[0] * R, todo[1], partial))
             fixed += 1
         tot = IDENT
         for k in range(lo, hi):
@@ -203,7 +205,9 @@ def model_index(b, inject=None, order_seed=None, block=B):
         for i, p in enumerate(lst):
             nxt = lst[i + 1] if i + 1 < len(lst) else ex
             offs.append(p + 16)
-            lens.append(nxt - p - 16)
+            # (partial: a walk stopped by a record past the prefix's end left the region's exit at
+            # that end, so the emit reads the region's last incl_len from its header)
+            lens.append(u32(b, p + 8) if partial and i + 1 == len(lst) else nxt - p - 16)
     assert len(offs) == incl[-1][1]
     return np.array(offs, np.uint64), np.array(lens, np.uint32), fixed
 
@@ -279,3 +283,22 @@ def test_model_adjacent_wrong_guesses_any_chase_order():
         if trial % 4 == 1:  # a wrong guess pointing into the next region
             bad[a + 1] = (a + 2) * R + 17
         check(b, inject=bad, order_seed=trial, block=(5, 8, 256)[trial % 3])
+
+
+def test_model_prefixes_of_a_capture():
+    """pkt_parse_pcap_host's pieces: the index of a PREFIX of a capture (partial mode) is exactly the
+    records wholly inside it — the full index's first m records, m = those whose data end lies within
+    the prefix — for cuts inside record headers, inside record data and at record boundaries, with
+    wrong guesses injected and look-backs in any order."""
+    buf, _, _ = gen.gen_c4(2500, seed=21)
+    b = buf.tobytes()
+    o_full, l_full = gen.pcap_index_py(b)
+    ends = o_full.astype(np.int64) + l_full.astype(np.int64)
+    rng = np.random.default_rng(5)
+    cuts = [24, 40, 4096, 4097] + [int(x) for x in rng.integers(24, len(b), 14)] + \
+           [int(o_full[7]) - 16, int(o_full[7]) - 9, int(ends[100]), int(ends[100]) + 1, len(b)]
+    for i, cut in enumerate(cuts):
+        m = int((ends <= cut).sum())
+        o, l, _ = model_index(b[:cut], order_seed=i, block=4, partial=True,
+                              inject={3: 3 * R + 1} if cut > 5 * R else None)
+        assert np.array_equal(o, o_full[:m]) and np.array_equal(l, l_full[:m]), (cut, m, len(o))
