@@ -1051,7 +1051,9 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         (void)hipFree(ctx->hp.ioffs);
         (void)hipFree(ctx->hp.ilens);
         (void)hipFree(ctx->hp.pcnt);
-        for (uint32_t k = 0; k < ctx->hp.pev_n; k++) (void)hipEventDestroy(ctx->hp.pev[k]);
+        (void)hipFree(ctx->hp.pnh);
+        (void)hipFree(ctx->hp.dcol);
+        for (uint32_t k = 0; k < 2 * ctx->hp.pev_n; k++) (void)hipEventDestroy(ctx->hp.pev[k]);
         delete[] ctx->hp.pev;
     }
     delete ctx;
@@ -1581,51 +1583,92 @@ int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
 
 constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
 
-// pkt_parse_pcap_host with pinned columns, piece by piece (include/pktgpu.h): piece k's copy on hp.s[1];
-// on hp.s[0], once it has landed, the index of the prefix [0, hi_k) (partial: a record running past hi_k
-// is left to a later prefix; the last prefix is the file, with the errors) writing its record count to
-// count word k, and the parse of records [count k-1, count k) writing the pinned columns over the link
-// while the next pieces copy in.  The records a prefix adds all end in (hi_{k-1}, hi_k] and are disjoint
-// (>= 16 B each), so at most (hi_k - hi_{k-1}) / 16 + 1 of them: that sizes each parse's grid.
-static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t& dout,
-                            uint64_t* offsets, uint32_t* lens, uint64_t cap, uint64_t* n_out, uint64_t piece) {
+// pkt_parse_pcap_host with pinned columns, piece by piece (include/pktgpu.h), on the ctx's three host
+// streams: hp.s[1] copies piece k in; hp.s[0], once it has landed, indexes the prefix [0, hi_k)
+// (partial: a record running past hi_k is left to a later prefix; the last prefix is the file, with
+// the errors) into count word k and parses records [count k-1, count k) into DEVICE columns (the
+// caller's layout: slot rows strided by cap), reducing the piece's largest n_hdrs; hp.s[2] then exports
+// those records' column ranges to the caller's pinned columns in 16-byte chunks (export_kernel,
+// pktgpu_gather.hip) while the next pieces copy in — the link is full duplex.  The parse kernel writing
+// the host columns itself (its 1-8 B per-lane stores over the link) moved them at ~21 GB/s against
+// ~57 GB/s for wide chunks (profiles/host/r05b_pcap_host_pieces.jsonl).  The records a prefix adds all
+// end in (hi_{k-1}, hi_k] and are disjoint (>= 16 B each): at most (hi_k - hi_{k-1}) / 16 + 1 of them,
+// which sizes each parse's grid.
+static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                            const pkt_out_t& hout, uint64_t* offsets, uint32_t* lens, uint64_t cap,
+                            uint64_t* n_out, uint64_t piece) {
     HostPipe& hp = ctx->hp;
-    hipStream_t cs = hp.s[1], ps = hp.s[0];
+    hipStream_t cs = hp.s[1], ps = hp.s[0], es = hp.s[2];
     const uint64_t np64 = (len + piece - 1) / piece;
     if (np64 > (1u << 20)) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host: too many pieces");
     const uint32_t np = (uint32_t)np64;
     hipError_t e = hipSuccess;
     if (np > hp.pcnt_cap) {
         (void)hipFree(hp.pcnt);
+        (void)hipFree(hp.pnh);
         hp.pcnt = nullptr;
+        hp.pnh = nullptr;
         hp.pcnt_cap = 0;
-        if ((e = hipMalloc(reinterpret_cast<void**>(&hp.pcnt), (uint64_t)np * 8)) != hipSuccess)
-            return hip_fail(ctx, e, "hipMalloc (piece counts)");
+        e = hipMalloc(reinterpret_cast<void**>(&hp.pcnt), (uint64_t)np * 8);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&hp.pnh), (uint64_t)np * kMaxSpread * 4);
+        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (piece counts)");
         hp.pcnt_cap = np;
     }
     if (np > hp.pev_n) {
-        hipEvent_t* ev = new hipEvent_t[np]();
-        for (uint32_t k = 0; k < hp.pev_n; k++) ev[k] = hp.pev[k];
+        hipEvent_t* ev = new hipEvent_t[2 * (size_t)np]();
+        for (uint32_t k = 0; k < 2 * hp.pev_n; k++) ev[k] = hp.pev[k];
         delete[] hp.pev;
         hp.pev = ev;
         for (uint32_t k = hp.pev_n; k < np && e == hipSuccess; k++) {
-            e = hipEventCreateWithFlags(&hp.pev[k], hipEventDisableTiming);
+            e = hipEventCreateWithFlags(&hp.pev[2 * k], hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&hp.pev[2 * k + 1], hipEventDisableTiming);
             if (e == hipSuccess) hp.pev_n = k + 1;
         }
         if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate (pieces)");
+    }
+    // the device columns: the requested ones, each at a 256-byte boundary, the caller's shapes
+    const uint8_t* const* hcol = reinterpret_cast<const uint8_t* const*>(out);
+    uint64_t coff[49], need = 0;
+    for (int c = 0; c < 49; c++) {
+        coff[c] = need;
+        if (hcol[c]) need += (col_bytes(c, cap) + 255) & ~(uint64_t)255;
+    }
+    if (need > hp.dcol_cap) {
+        (void)hipFree(hp.dcol);
+        hp.dcol = nullptr;
+        hp.dcol_cap = 0;
+        if ((e = hipMalloc(reinterpret_cast<void**>(&hp.dcol), need)) != hipSuccess)
+            return hip_fail(ctx, e, "hipMalloc (capture columns)");
+        hp.dcol_cap = need;
+    }
+    pkt_out_t dcols;
+    uint8_t** dc = reinterpret_cast<uint8_t**>(&dcols);
+    const uint8_t* const* hc = reinterpret_cast<const uint8_t* const*>(&hout);  // device-mapped host columns
+    ExportArgs xa;
+    xa.ncol = 0;
+    xa.cap = cap;
+    for (int c = 0; c < 49; c++) {
+        dc[c] = hcol[c] ? hp.dcol + coff[c] : nullptr;
+        if (!hcol[c]) continue;
+        const bool slot = c == kColHdrType || c == kColHdrOff;
+        for (uint32_t r = 0; r < (slot ? (uint32_t)PKT_MAX_HDRS : 1u); r++)
+            xa.col[xa.ncol++] = ExportCol{reinterpret_cast<uint64_t>(dc[c]) + (uint64_t)r * cap * kColSize[c],
+                                          reinterpret_cast<uint64_t>(hc[c]) + (uint64_t)r * cap * kColSize[c],
+                                          kColSize[c], slot ? r : kExportNoRow};
     }
     int rc = pktgpu_pcap_reserve(ctx, len, ps);  // the whole file's scratch: no growth between prefixes
     if (rc != PKT_SUCCESS) return rc;
     auto bail = [&](int code) {  // nothing left in flight that reads `buf` or writes `out`
         (void)hipStreamSynchronize(cs);
         (void)hipStreamSynchronize(ps);
+        (void)hipStreamSynchronize(es);
         return code;
     };
     uint64_t hi_prev = 0;
     for (uint32_t k = 0; k < np; k++) {
         const uint64_t lo = (uint64_t)k * piece, hi = std::min(len, lo + piece);
         if ((e = hipMemcpyAsync(hp.file + lo, buf + lo, hi - lo, hipMemcpyHostToDevice, cs)) != hipSuccess ||
-            (e = hipEventRecord(hp.pev[k], cs)) != hipSuccess || (e = hipStreamWaitEvent(ps, hp.pev[k], 0)) != hipSuccess)
+            (e = hipEventRecord(hp.pev[2 * k], cs)) != hipSuccess || (e = hipStreamWaitEvent(ps, hp.pev[2 * k], 0)) != hipSuccess)
             return bail(hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap piece)"));
         const bool last = k + 1 == np;
         const uint64_t* cnt = nullptr;
@@ -1639,19 +1682,28 @@ static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, in
         db.stride = 0;
         db.reserved = 0;
         db.n = cap;
-        rc = parse_impl(ctx, &db, entry, &dout, ps, 0, ctx->staging, nullptr, cap, nullptr, cnt,
+        uint32_t* nh = hp.pnh + (uint64_t)k * kMaxSpread;
+        if ((e = hipMemsetAsync(nh, 0, kMaxSpread * 4, ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMemsetAsync"));
+        rc = parse_impl(ctx, &db, entry, &dcols, ps, 0, ctx->staging, nh, cap, nullptr, cnt,
                         k ? hp.pcnt + (k - 1) : nullptr, (hi - hi_prev) / 16 + 1);
         if (rc != PKT_SUCCESS) return bail(rc);
+        if ((e = hipEventRecord(hp.pev[2 * k + 1], ps)) != hipSuccess || (e = hipStreamWaitEvent(es, hp.pev[2 * k + 1], 0)) != hipSuccess)
+            return bail(hip_fail(ctx, e, "hipEventRecord (piece parsed)"));
+        xa.lo_dev = k ? hp.pcnt + (k - 1) : nullptr;
+        xa.hi_dev = cnt;
+        xa.nhw = nh;
+        if ((e = pktgpu_export_launch(xa, es)) != hipSuccess) return bail(hip_fail(ctx, e, "export_kernel"));
         hi_prev = hi;
     }
     if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
-    if ((rc = pktgpu_pcap_finish(ctx, n_out)) != PKT_SUCCESS) return rc;
+    if ((rc = pktgpu_pcap_finish(ctx, n_out)) != PKT_SUCCESS) return bail(rc);
     const uint64_t m = std::min(*n_out, cap);
-    if (m && offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, ps)) != hipSuccess)
+    if (m && offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, cs)) != hipSuccess)
         return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)"));
-    if (m && lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, ps)) != hipSuccess)
+    if (m && lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, cs)) != hipSuccess)
         return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)"));
-    if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
+    if ((e = hipStreamSynchronize(cs)) != hipSuccess || (e = hipStreamSynchronize(es)) != hipSuccess)
+        return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
     return PKT_SUCCESS;
 }
 
@@ -1667,11 +1719,11 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
     hipStream_t s = hp.s[0];
-    {  // pinned columns and more than one piece: copy, index and parse piece by piece
+    {  // pinned columns: copy, index, parse and export piece by piece (one piece for a short file)
         pkt_out_t dout;
         const uint64_t piece = ctx->host_piece ? ctx->host_piece : kHostPiece;
-        if (len > piece && cap && cap <= kLaunchChunk && out_mapped(out, dout))
-            return pcap_host_pieces(ctx, buf, len, entry, dout, offsets, lens, cap, n_out, piece);
+        if (len >= 24 && cap && cap <= kLaunchChunk && out_mapped(out, dout))
+            return pcap_host_pieces(ctx, buf, len, entry, out, dout, offsets, lens, cap, n_out, piece);
     }
     // every error return after the first queued copy waits for the ctx's streams first: a copy from
     // `buf` or into `offsets` / `lens` must not outlive the call

@@ -28,8 +28,11 @@ struct HostPipe {
     // the piece's end), one copy-done event per piece
     uint64_t* pcnt = nullptr;
     uint32_t pcnt_cap = 0;
-    hipEvent_t* pev = nullptr;
+    hipEvent_t* pev = nullptr;   // [2 * pev_n]: piece k landed (pev[2k]), piece k parsed (pev[2k + 1])
     uint32_t pev_n = 0;
+    uint32_t* pnh = nullptr;     // [pcnt_cap][256]: each piece's n_hdrs maximum, spread
+    uint8_t* dcol = nullptr;     // the capture's columns on the device (the export's source)
+    uint64_t dcol_cap = 0;       // bytes
 };
 
 // Per-region state of the device pcap indexer (pkt_pcap_index_device), grown on demand.
@@ -146,3 +149,23 @@ struct RepackPiece {
 };
 uint32_t pktgpu_repack_blocks(uint64_t bytes);
 hipError_t pktgpu_repack_launch(const RepackPiece* tab_dev, uint32_t np, uint32_t nblocks, hipStream_t s);
+
+// pkt_parse_pcap_host's column export (pktgpu_gather.hip): column range y copies elements [*lo_dev (NULL:
+// 0), min(*hi_dev, cap)) of `sz` bytes from device address src to the host column dst (device-mapped);
+// a slot row (row != kExportNoRow) only below the largest of the 256 words at nhw.
+constexpr uint32_t kExportNoRow = 0xFFFFu;
+constexpr int kExportMax = 80;   // 47 per-packet columns + 2 x 16 slot rows
+constexpr int kExportParts = 32; // blocks per column range
+struct ExportCol {
+    uint64_t src, dst;
+    uint32_t sz, row;
+};
+struct ExportArgs {
+    ExportCol col[kExportMax];
+    const uint64_t* lo_dev;
+    const uint64_t* hi_dev;
+    const uint32_t* nhw;
+    uint64_t cap;
+    uint32_t ncol;
+};
+hipError_t pktgpu_export_launch(const ExportArgs& a, hipStream_t s);

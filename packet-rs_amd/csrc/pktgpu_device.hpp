@@ -148,9 +148,6 @@ __device__ __forceinline__ void dispatch_init(DispatchLds* T, uint32_t t, uint32
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-#ifndef PKTGPU_LE_X2
-#define PKTGPU_LE_X2 1  // PacketView::le past the window: one 8-byte load instead of two dword loads
-#endif
 // A lane's view of its packet: LDS window + global fallback.
 struct PacketView {
     const uint8_t* lw;        // LDS window of this packet (dword-aligned)
@@ -184,17 +181,8 @@ struct PacketView {
         }
         const uint64_t a = off + b;
         const uint32_t sh = (uint32_t)(a & 3);
-#if PKTGPU_LE_X2
-        // both dwords by ONE 8-byte load at the 4-byte-aligned address (global_load_dwordx2): two
-        // dword loads are two instructions, and separate instructions to one 128-B line re-request it
-        // from memory
-        const uint64_t d = a & ~(uint64_t)3;
-        if (d + 4 <= last4) {
-            uint32_t v[2];
-            __builtin_memcpy(v, __builtin_assume_aligned(slab + d, 4), 8);
-            return __builtin_amdgcn_alignbyte(v[1], v[0], sh);
-        }
-#endif
+        // (one 8-byte load at the 4-byte-aligned address instead of the two dword loads changed
+        // neither the C4 reads nor the time: profiles/ab/r05b_c4_le_dwordx2.txt)
         const uint32_t lo = gdw(a);
         const uint32_t hi = (sh + n > 4) ? gdw(a + 4) : 0u;
         return __builtin_amdgcn_alignbyte(hi, lo, sh);

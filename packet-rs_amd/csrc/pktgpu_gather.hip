@@ -88,3 +88,71 @@ hipError_t pktgpu_repack_launch(const RepackPiece* tab_dev, uint32_t np, uint32_
     hipLaunchKernelGGL(repack_kernel, dim3(nblocks), dim3(256), 0, s, tab_dev, np);
     return hipGetLastError();
 }
+
+// ---- the capture-in-host-memory path's column export (pkt_parse_pcap_host, pktgpu.hip) ----
+// A piece's records [lo, hi) (device words: the prefix counts) were parsed into DEVICE columns laid out
+// like the caller's host columns (same element size, slot rows strided by cap); this kernel copies each
+// column's range [lo, hi) — each slot row's below the piece's largest n_hdrs — into the caller's pinned
+// host columns over the link.  16-byte chunks by consecutive lanes, so a wave instruction writes 1 KiB
+// of one column: the parse's own per-lane stores to host memory (1-8 B per lane, 64-512 B per wave
+// instruction) moved the columns at ~21 GB/s, a copy of wide chunks at the link's rate (~57 GB/s,
+// profiles/host/r05b_pcap_host_pieces.jsonl).  Block (x, y): part x of column range y.
+namespace {
+__global__ __launch_bounds__(256) void export_kernel(ExportArgs a) {
+    const ExportCol c = a.col[blockIdx.y];
+    uint64_t hi = *a.hi_dev, lo = a.lo_dev ? *a.lo_dev : 0;
+    hi = hi < a.cap ? hi : a.cap;
+    lo = lo < hi ? lo : hi;
+    const uint32_t t = threadIdx.x;
+    if (c.row != kExportNoRow) {  // a slot row: only below the piece's largest n_hdrs (256 spread words)
+        __shared__ uint32_t s_max[4];
+        uint32_t m = a.nhw[t];
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, d, 64));
+        if ((t & 63u) == 0) s_max[t >> 6] = m;
+        __syncthreads();
+        m = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+        if (c.row >= m) return;
+    }
+    const uint64_t bytes = (hi - lo) * c.sz;
+    if (!bytes) return;
+    const uint8_t* s = reinterpret_cast<const uint8_t*>(c.src) + lo * c.sz;
+    uint8_t* d = reinterpret_cast<uint8_t*>(c.dst) + lo * c.sz;
+    const uint64_t lead = (uint64_t)(-(int64_t)reinterpret_cast<uintptr_t>(d)) & 15u;
+    const uint64_t head = lead < bytes ? lead : bytes;
+    const uint64_t nb = (bytes - head) >> 4, body_end = head + 16u * nb;
+    if (blockIdx.x == 0) {
+        if (t < head) d[t] = s[t];
+        if (t < bytes - body_end) d[body_end + t] = s[body_end + t];
+    }
+    const uint8_t* sb = s + head;
+    uint4* db = reinterpret_cast<uint4*>(d + head);
+    const uint64_t step = (uint64_t)gridDim.x * 256u;
+    if ((reinterpret_cast<uintptr_t>(sb) & 15u) == 0) {
+        for (uint64_t k = (uint64_t)blockIdx.x * 256u + t; k < nb; k += 2 * step) {
+            const uint4 v0 = reinterpret_cast<const uint4*>(sb)[k];
+            const bool two = k + step < nb;
+            uint4 v1 = v0;
+            if (two) v1 = reinterpret_cast<const uint4*>(sb)[k + step];
+            db[k] = v0;
+            if (two) db[k + step] = v1;
+        }
+    } else {
+        for (uint64_t k = (uint64_t)blockIdx.x * 256u + t; k < nb; k += step) {
+            uint32_t w[4];
+            const uint8_t* b = sb + 16u * k;
+#pragma unroll
+            for (int q = 0; q < 4; q++)
+                w[q] = (uint32_t)b[4 * q] | ((uint32_t)b[4 * q + 1] << 8) | ((uint32_t)b[4 * q + 2] << 16) |
+                       ((uint32_t)b[4 * q + 3] << 24);
+            db[k] = make_uint4(w[0], w[1], w[2], w[3]);
+        }
+    }
+}
+}  // namespace
+
+hipError_t pktgpu_export_launch(const ExportArgs& a, hipStream_t s) {
+    if (!a.ncol) return hipSuccess;
+    hipLaunchKernelGGL(export_kernel, dim3(kExportParts, a.ncol), dim3(256), 0, s, a);
+    return hipGetLastError();
+}

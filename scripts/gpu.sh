@@ -20,6 +20,7 @@
 #   pcapstamps         guess-wave / scan-block segment stamps (lib/variants/stamps.so, scripts/pcap_stamps.py)
 #   secondary          §8(f) kernels: scripts/secondary_bench.py + rocprofv3 kernel stats
 #   host               host-memory path rates (scripts/hostpath_native.py, pinned and pageable)
+#   hostpieces[=LIST]  pkt_parse_pcap_host by piece size + the link alone (scripts/pcap_host_pieces.py)
 #   ab=CFGS:VARS       every lib/variants/*.so through kbench, interleaved (scripts/ab.sh)
 #   abn=CFG:VARS:A,B   named builds (main = lib/libpktgpu.so, else lib/variants/NAME.so), kbench, 3 rounds
 #   pcapn=A,B          named builds through scripts/pcap_index_bench.py, 3 interleaved rounds
@@ -72,6 +73,7 @@ for step in "$@"; do
     secondary) run secondary 300 python scripts/secondary_bench.py
            run secondary_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/secprof" -o trace -- \
                python scripts/secondary_bench.py --cpu-budget 0.2 ;;
+    hostpieces) run hostpieces 300 python scripts/pcap_host_pieces.py ${arg:+--pieces $arg} ;;
     host)  run host 600 bash -c 'for c in c2 c4; do python scripts/hostpath_native.py --config $c --chunks 262144 || exit $?;
                python scripts/hostpath_native.py --config $c --pageable --chunks 131072,262144 || exit $?; done' ;;
     ab)    IFS=: read -r c v <<< "$arg"; run ab_${c:-c2} 900 bash scripts/ab.sh "${c:-c2}" "${v:-status;chain;all}" 2 ;;
