@@ -296,13 +296,15 @@ int pkt_parse_batches(pkt_ctx_t *ctx, const pkt_batch_t *batches, uint32_t nbatc
  * The reference's path starts and ends in host memory (a pcap file, a NIC ring).  One call moves
  * a HOST batch through the device: `batch` (slab, offsets, lens) and `out` (column pointers, the
  * pkt_out_t layout of pkt_parse_batch with slot columns strided by batch->n) are host memory.
- * The batch is cut into chunks of `chunk` packets (0 = 262144) pipelined over three streams of
- * the ctx: the copy-in of chunk k+1 and the copy-out of chunk k-1 overlap the parse of chunk k.
- * Indexed chunks copy the byte span their records cover.  When the slab, offsets, lens and every
- * requested column are pinned memory from pkt_host_alloc, there are no copies at all: one launch
- * reads the slab and writes the columns over the link directly (zero copy; `chunk` unused).
- * Pageable buffers work, staged by the runtime.  Blocks until every output is in host memory.
- * One host call at a time per ctx. */
+ * The batch is cut into chunks of `chunk` packets (0 = 262144; 131072 with pinned columns)
+ * pipelined over three streams of the ctx: the copy-in of chunk k+1 and the copy-out of chunk k-1
+ * overlap the parse of chunk k.  Indexed chunks copy the byte span their records cover.  When every
+ * requested column is pinned memory from pkt_host_alloc, a chunk's columns go out by one kernel
+ * writing them over the link in 16-byte chunks (else one copy per column).  With
+ * pkt_ctx_set_staging(2) and the slab, offsets, lens and columns all pinned: zero copy — one launch
+ * reads the slab and writes the columns over the link directly (`chunk` unused).  Pageable buffers
+ * work, staged by the runtime.  Blocks until every output is in host memory.  One host call at a
+ * time per ctx. */
 int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pkt_out_t *out,
                    uint64_t chunk);
 /* The capture path of tests/pcap.rs:7-37 end to end, host memory in and out: a pcap file in HOST
@@ -323,12 +325,13 @@ int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pk
 int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                         uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out);
 /* pkt_parse_pcap_host without the wait, for a stream of captures (cap <= 2^26, every column of `out`
- * in pinned memory from pkt_host_alloc, no index output): queues the file's copy in, the index and
- * the parse (whose kernel writes the columns over the link) on the ctx's own stream and returns;
- * `buf` and `out` must stay untouched until pkt_parse_pcap_host_result, which waits for them and
- * gives the outcome as pkt_parse_pcap_host's (*n_out = the record count).  One capture in flight
- * per ctx (as pkt_parse_pcap_async): two ctxs keep one capture's copy in flowing while the other's
- * columns flow out. */
+ * in pinned memory from pkt_host_alloc, no index output): queues pkt_parse_pcap_host's pieces — the
+ * copies in, the prefix indexes, the parses and the column exports — on the ctx's own streams and
+ * returns; `buf` and `out` must stay untouched until pkt_parse_pcap_host_result, which waits for them
+ * and gives the outcome as pkt_parse_pcap_host's (*n_out = the record count; on an error in the last
+ * record the earlier pieces' records may be written).  One capture in flight per ctx (as
+ * pkt_parse_pcap_async): two ctxs keep one capture's copy in flowing while the other's columns flow
+ * out. */
 int pkt_parse_pcap_host_async(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                               uint64_t cap);
 int pkt_parse_pcap_host_result(pkt_ctx_t *ctx, uint64_t *n_out);

@@ -1292,12 +1292,15 @@ int pkt_host_free(pkt_ctx_t* ctx, void* p) {
 // once the chunk's n_hdrs maximum, reduced inside its parse, is known — one chunk later, so the host
 // never waits on the chunk it has just queued).  dev_in = false: `b` is host memory and each chunk's
 // bytes (+ offsets / lens) are copied in first; dev_in = true: `b` is already in device memory.
+// hout (non-NULL: every requested host column is pinned, these are their device-mapped addresses): each
+// chunk's columns leave by one export_kernel launch writing 16-byte chunks over the link (pktgpu_gather.hip)
+// instead of one DMA copy per column — ~30 small copies per chunk, each with its own setup.
 static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_out_t* out, uint64_t chunk,
-                        bool dev_in, uint64_t slot_stride = 0) {
+                        bool dev_in, uint64_t slot_stride = 0, const pkt_out_t* hout = nullptr) {
     HostPipe& hp = ctx->hp;
     hipError_t e = hipSuccess;
     const uint64_t n = b->n, hstride = slot_stride ? slot_stride : n;  // host slot rows: [16][hstride]
-    const uint64_t cn = std::min<uint64_t>(chunk ? chunk : (1ull << 18), n);
+    const uint64_t cn = std::min<uint64_t>(chunk ? chunk : (hout ? (1ull << 17) : (1ull << 18)), n);
     const uint64_t nchunks = (n + cn - 1) / cn;
 
     // bytes of input each chunk needs on the device (indexed: the span its records cover,
@@ -1417,6 +1420,30 @@ static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const p
         }
         rc = parse_impl(ctx, &db, entry, &dout, s, bias, ctx->staging, slot_rows ? ctx->mx.dgroup(q) : nullptr);
         if (rc != PKT_SUCCESS) break;
+        if (hout) {  // every column of the chunk by one export launch (slot rows up to the chunk's n_hdrs max)
+            ExportArgs xa;
+            xa.ncol = 0;
+            xa.lo_dev = xa.hi_dev = nullptr;
+            xa.lo_h = 0;
+            xa.hi_h = m;
+            xa.cap = m;
+            xa.nhw = slot_rows ? ctx->mx.dgroup(q) : nullptr;
+            const uint8_t* const* hm = reinterpret_cast<const uint8_t* const*>(hout);
+            for (int c = 0; c < 49; c++) {
+                if (!hcol[c]) continue;
+                const bool slot = c == kColHdrType || c == kColHdrOff;
+                const uint64_t sz = kColSize[c];
+                for (uint32_t r = 0; r < (slot ? (uint32_t)PKT_MAX_HDRS : 1u); r++)
+                    xa.col[xa.ncol++] = ExportCol{reinterpret_cast<uint64_t>(dcol[c]) + (uint64_t)r * m * sz,
+                                                  reinterpret_cast<uint64_t>(hm[c]) + ((uint64_t)r * hstride + lo) * sz,
+                                                  (uint32_t)sz, slot ? r : kExportNoRow};
+            }
+            if ((e = pktgpu_export_launch(xa, s)) != hipSuccess) {
+                rc = hip_fail(ctx, e, "export_kernel");
+                break;
+            }
+            continue;
+        }
         // out: every requested per-packet column into its host rows [lo, hi); the slot rows of this
         // chunk once its count is known (after the next chunk is queued)
         for (int c = 0; c < 49 && e == hipSuccess; c++) {
@@ -1432,7 +1459,7 @@ static int staged_parse(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const p
         if (e == hipSuccess && k > 0) e = copy_slots(k - 1);
         if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMemcpyAsync D2H");
     }
-    if (rc == PKT_SUCCESS && nchunks > 0) {
+    if (rc == PKT_SUCCESS && nchunks > 0 && !hout) {
         e = copy_slots(nchunks - 1);
         if (e != hipSuccess) rc = hip_fail(ctx, e, "hipMemcpyAsync D2H");
     }
@@ -1478,14 +1505,19 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     int rc = host_pipe_init(ctx);
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
-    // Zero copy: when the slab, the index arrays and every requested column are pinned host memory
-    // mapped into the device (pkt_host_alloc), the kernel reads and writes them over PCIe directly —
-    // one launch, no staging copies, both link directions busy at once.
+    // Pinned columns (pkt_host_alloc): chunks copied in by DMA on the pipeline's streams, parsed on the
+    // device, and each chunk's columns exported by one kernel writing 16-byte chunks over the link while
+    // the next chunks copy in (staged_parse with hout).  Zero copy — the parse kernel reading the pinned
+    // slab and writing the pinned columns over PCIe itself, one launch — when asked for with
+    // pkt_ctx_set_staging(2): its 1-8 B per-lane column stores keep the link at ~21-39 GB/s out
+    // (DESIGN.md §7).
     {
         pkt_batch_t db = *b;
         pkt_out_t dout;
-        const bool mapped = host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
-                            (!b->lens || host_mapped(b->lens, db.lens)) && out_mapped(out, dout);
+        const bool omap = out_mapped(out, dout);
+        const bool mapped = omap && host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
+                            (!b->lens || host_mapped(b->lens, db.lens));
+        if (!(mapped && ctx->staging == 2) && omap) return staged_parse(ctx, b, entry, out, chunk, false, 0, &dout);
         if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
             // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
             // for a deep header (per-lane windows would, one dependent PCIe read each)
@@ -1535,6 +1567,11 @@ static int pcap_host_buffers(pkt_ctx_t* ctx, uint64_t len, uint64_t cap) {
     return PKT_SUCCESS;
 }
 
+static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
+                            const pkt_out_t& hout, uint64_t* offsets, uint32_t* lens, uint64_t cap,
+                            uint64_t* n_out, uint64_t piece, bool blocking);
+constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
+
 extern "C" {
 
 int pkt_parse_pcap_host_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
@@ -1547,41 +1584,29 @@ int pkt_parse_pcap_host_async(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, 
         return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host_async: the columns must be pinned (pkt_host_alloc)");
     int rc = pcap_host_buffers(ctx, len, cap);
     if (rc != PKT_SUCCESS) return rc;
-    HostPipe& hp = ctx->hp;
-    hipStream_t s = hp.s[0];
-    hipError_t e = hipMemcpyAsync(hp.file, buf, len, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap file)");
-    const uint64_t* count_dev = nullptr;
-    if ((rc = pktgpu_pcap_launch(ctx, hp.file, len, hp.ioffs, hp.ilens, cap, s, &count_dev)) != PKT_SUCCESS) {
-        (void)hipStreamSynchronize(s);  // the copy queued above may still be reading `buf`
-        return rc;
-    }
-    pkt_batch_t db;
-    db.slab = hp.file;
-    db.slab_len = len;
-    db.offsets = hp.ioffs;
-    db.lens = hp.ilens;
-    db.stride = 0;
-    db.reserved = 0;
-    db.n = cap;  // blocks past the device-produced count exit
-    if ((rc = parse_impl(ctx, &db, entry, &dout, s, 0, ctx->staging, nullptr, cap, nullptr, count_dev)) != PKT_SUCCESS) {
-        (void)hipStreamSynchronize(s);  // nothing left in flight
-        return rc;
-    }
-    ctx->pc.pending = true;
-    ctx->pc.pending_stream = s;
-    return PKT_SUCCESS;
+    if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
+    uint64_t n_unused = 0;
+    // the blocking call's pieces, queued on the ctx's three streams (pkt_parse_pcap_host_result waits)
+    return pcap_host_pieces(ctx, buf, len, entry, out, dout, nullptr, nullptr, cap, &n_unused,
+                            ctx->host_piece ? ctx->host_piece : kHostPiece, false);
 }
 
 int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
     if (!ctx || !n_out) return fail(ctx, PKT_ERR_INVALID_ARG, "null argument");
     *n_out = 0;
+    if (ctx->pc.pending && ctx->hp.init) {  // the copy and export streams of the queued capture
+        (void)hipSetDevice(ctx->device);
+        const hipError_t e1 = hipStreamSynchronize(ctx->hp.s[1]), e2 = hipStreamSynchronize(ctx->hp.s[2]);
+        if (e1 != hipSuccess || e2 != hipSuccess) {
+            uint64_t ignored = 0;
+            (void)pktgpu_pcap_take(ctx, &ignored);
+            return hip_fail(ctx, e1 != hipSuccess ? e1 : e2, "pkt_parse_pcap_host_result");
+        }
+    }
     return pktgpu_pcap_take(ctx, n_out);
 }
 
 }  // extern "C"
-
-constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
 
 // pkt_parse_pcap_host with pinned columns, piece by piece (include/pktgpu.h), on the ctx's three host
 // streams: hp.s[1] copies piece k in; hp.s[0], once it has landed, indexes the prefix [0, hi_k)
@@ -1594,9 +1619,10 @@ constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default by
 // ~57 GB/s for wide chunks (profiles/host/r05b_pcap_host_pieces.jsonl).  The records a prefix adds all
 // end in (hi_{k-1}, hi_k] and are disjoint (>= 16 B each): at most (hi_k - hi_{k-1}) / 16 + 1 of them,
 // which sizes each parse's grid.
+// blocking = false (pkt_parse_pcap_host_async): everything queued, the capture left pending on the ctx.
 static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
                             const pkt_out_t& hout, uint64_t* offsets, uint32_t* lens, uint64_t cap,
-                            uint64_t* n_out, uint64_t piece) {
+                            uint64_t* n_out, uint64_t piece, bool blocking) {
     HostPipe& hp = ctx->hp;
     hipStream_t cs = hp.s[1], ps = hp.s[0], es = hp.s[2];
     const uint64_t np64 = (len + piece - 1) / piece;
@@ -1647,6 +1673,7 @@ static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, in
     ExportArgs xa;
     xa.ncol = 0;
     xa.cap = cap;
+    xa.lo_h = xa.hi_h = 0;
     for (int c = 0; c < 49; c++) {
         dc[c] = hcol[c] ? hp.dcol + coff[c] : nullptr;
         if (!hcol[c]) continue;
@@ -1695,6 +1722,11 @@ static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, in
         if ((e = pktgpu_export_launch(xa, es)) != hipSuccess) return bail(hip_fail(ctx, e, "export_kernel"));
         hi_prev = hi;
     }
+    if (!blocking) {
+        ctx->pc.pending = true;
+        ctx->pc.pending_stream = ps;
+        return PKT_SUCCESS;
+    }
     if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
     if ((rc = pktgpu_pcap_finish(ctx, n_out)) != PKT_SUCCESS) return bail(rc);
     const uint64_t m = std::min(*n_out, cap);
@@ -1723,7 +1755,7 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
         pkt_out_t dout;
         const uint64_t piece = ctx->host_piece ? ctx->host_piece : kHostPiece;
         if (len >= 24 && cap && cap <= kLaunchChunk && out_mapped(out, dout))
-            return pcap_host_pieces(ctx, buf, len, entry, out, dout, offsets, lens, cap, n_out, piece);
+            return pcap_host_pieces(ctx, buf, len, entry, out, dout, offsets, lens, cap, n_out, piece, true);
     }
     // every error return after the first queued copy waits for the ctx's streams first: a copy from
     // `buf` or into `offsets` / `lens` must not outlive the call

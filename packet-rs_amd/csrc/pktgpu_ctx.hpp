@@ -150,9 +150,10 @@ struct RepackPiece {
 uint32_t pktgpu_repack_blocks(uint64_t bytes);
 hipError_t pktgpu_repack_launch(const RepackPiece* tab_dev, uint32_t np, uint32_t nblocks, hipStream_t s);
 
-// pkt_parse_pcap_host's column export (pktgpu_gather.hip): column range y copies elements [*lo_dev (NULL:
-// 0), min(*hi_dev, cap)) of `sz` bytes from device address src to the host column dst (device-mapped);
-// a slot row (row != kExportNoRow) only below the largest of the 256 words at nhw.
+// The host paths' column export (pktgpu_gather.hip): column range y copies elements [*lo_dev (NULL: 0),
+// min(*hi_dev, cap)) — or [lo_h, hi_h) when hi_dev is NULL — of `sz` bytes from device address src + lo *
+// sz to the host column dst + lo * sz (device-mapped); a slot row (row != kExportNoRow) only below the
+// largest of the 256 words at nhw (NULL: every row).
 constexpr uint32_t kExportNoRow = 0xFFFFu;
 constexpr int kExportMax = 80;   // 47 per-packet columns + 2 x 16 slot rows
 constexpr int kExportParts = 32; // blocks per column range
@@ -162,9 +163,10 @@ struct ExportCol {
 };
 struct ExportArgs {
     ExportCol col[kExportMax];
-    const uint64_t* lo_dev;
+    const uint64_t* lo_dev;  // NULL with hi_dev NULL: the host-known range [lo_h, hi_h)
     const uint64_t* hi_dev;
-    const uint32_t* nhw;
+    const uint32_t* nhw;     // NULL: every slot row
+    uint64_t lo_h, hi_h;
     uint64_t cap;
     uint32_t ncol;
 };

@@ -100,11 +100,11 @@ hipError_t pktgpu_repack_launch(const RepackPiece* tab_dev, uint32_t np, uint32_
 namespace {
 __global__ __launch_bounds__(256) void export_kernel(ExportArgs a) {
     const ExportCol c = a.col[blockIdx.y];
-    uint64_t hi = *a.hi_dev, lo = a.lo_dev ? *a.lo_dev : 0;
+    uint64_t hi = a.hi_dev ? *a.hi_dev : a.hi_h, lo = a.hi_dev ? (a.lo_dev ? *a.lo_dev : 0) : a.lo_h;
     hi = hi < a.cap ? hi : a.cap;
     lo = lo < hi ? lo : hi;
     const uint32_t t = threadIdx.x;
-    if (c.row != kExportNoRow) {  // a slot row: only below the piece's largest n_hdrs (256 spread words)
+    if (c.row != kExportNoRow && a.nhw) {  // a slot row: only below the largest n_hdrs (256 spread words)
         __shared__ uint32_t s_max[4];
         uint32_t m = a.nhw[t];
 #pragma unroll
