@@ -298,13 +298,12 @@ int pkt_parse_batches(pkt_ctx_t *ctx, const pkt_batch_t *batches, uint32_t nbatc
  * pkt_out_t layout of pkt_parse_batch with slot columns strided by batch->n) are host memory.
  * The batch is cut into chunks of `chunk` packets (0 = 262144; 131072 with pinned columns)
  * pipelined over three streams of the ctx: the copy-in of chunk k+1 and the copy-out of chunk k-1
- * overlap the parse of chunk k.  Indexed chunks copy the byte span their records cover.  When every
- * requested column is pinned memory from pkt_host_alloc, a chunk's columns go out by one kernel
- * writing them over the link in 16-byte chunks (else one copy per column).  With
- * pkt_ctx_set_staging(2) and the slab, offsets, lens and columns all pinned: zero copy — one launch
- * reads the slab and writes the columns over the link directly (`chunk` unused).  Pageable buffers
- * work, staged by the runtime.  Blocks until every output is in host memory.  One host call at a
- * time per ctx. */
+ * overlap the parse of chunk k.  Indexed chunks copy the byte span their records cover.  When the
+ * slab, offsets, lens and every requested column are pinned memory from pkt_host_alloc, there are no
+ * copies at all: one launch reads the slab and writes the columns over the link directly (zero copy;
+ * `chunk` unused).  When only the columns are pinned, a chunk's columns go out by one kernel writing
+ * them over the link in 16-byte chunks (else one copy per column).  Pageable buffers work, staged by
+ * the runtime.  Blocks until every output is in host memory.  One host call at a time per ctx. */
 int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pkt_out_t *out,
                    uint64_t chunk);
 /* The capture path of tests/pcap.rs:7-37 end to end, host memory in and out: a pcap file in HOST

@@ -1505,19 +1505,21 @@ int pkt_parse_host(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt_ou
     int rc = host_pipe_init(ctx);
     if (rc != PKT_SUCCESS) return rc;
     HostPipe& hp = ctx->hp;
-    // Pinned columns (pkt_host_alloc): chunks copied in by DMA on the pipeline's streams, parsed on the
-    // device, and each chunk's columns exported by one kernel writing 16-byte chunks over the link while
-    // the next chunks copy in (staged_parse with hout).  Zero copy — the parse kernel reading the pinned
-    // slab and writing the pinned columns over PCIe itself, one launch — when asked for with
-    // pkt_ctx_set_staging(2): its 1-8 B per-lane column stores keep the link at ~21-39 GB/s out
-    // (DESIGN.md §7).
+    // Zero copy: when the slab, the index arrays and every requested column are pinned host memory
+    // mapped into the device (pkt_host_alloc), the kernel reads and writes them over PCIe directly —
+    // one launch, no staging copies, both link directions busy at once.  (Chunks copied
+    // in by DMA, parsed on the device and their columns exported by a kernel writing 16-byte chunks —
+    // the route the piecewise capture takes — measured slower here: C2 2.10 vs 1.86 ms, C4 6.63 vs
+    // 6.28 ms per 2^20 packets, profiles/host/r05e_host_export_vs_zero_copy.jsonl; it serves pinned
+    // columns of a pageable slab instead of one DMA copy per column.)
     {
         pkt_batch_t db = *b;
         pkt_out_t dout;
         const bool omap = out_mapped(out, dout);
         const bool mapped = omap && host_mapped(b->slab, db.slab) && (!b->offsets || host_mapped(b->offsets, db.offsets)) &&
                             (!b->lens || host_mapped(b->lens, db.lens));
-        if (!(mapped && ctx->staging == 2) && omap) return staged_parse(ctx, b, entry, out, chunk, false, 0, &dout);
+        if (omap && !(mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16))
+            return staged_parse(ctx, b, entry, out, chunk, false, 0, &dout);
         if (mapped && ((uintptr_t)db.slab & 15) == 0 && b->slab_len >= 16) {
             // wave spans read the link in 1-KiB contiguous pieces and never go back to host memory
             // for a deep header (per-lane windows would, one dependent PCIe read each)

@@ -20,6 +20,7 @@
 #   pcapstamps         guess-wave / scan-block segment stamps (lib/variants/stamps.so, scripts/pcap_stamps.py)
 #   secondary          §8(f) kernels: scripts/secondary_bench.py + rocprofv3 kernel stats
 #   host               host-memory path rates (scripts/hostpath_native.py, pinned and pageable)
+#   hostab             pkt_parse_host pinned: export pipeline vs zero copy, C2 and C4, by chunk
 #   hostpieces[=LIST]  pkt_parse_pcap_host by piece size + the link alone (scripts/pcap_host_pieces.py)
 #   ab=CFGS:VARS       every lib/variants/*.so through kbench, interleaved (scripts/ab.sh)
 #   abn=CFG:VARS:A,B   named builds (main = lib/libpktgpu.so, else lib/variants/NAME.so), kbench, 3 rounds
@@ -56,7 +57,7 @@ for step in "$@"; do
            run traffic_$c 60 python scripts/traffic.py "$OUT/pmc_fetch_$c" "$OUT/pmc_write_$c" "$OUT/traffic_$c.json" parse_kernel "$TAG $c" ;;
     kbench) IFS=: read -r c v w st <<< "$arg"
            run kbench_${c}_st${st:-0} 300 python scripts/kbench.py --config $c --variants "${v:-status;chain;all}" --windows ${w:-0} \
-               --staging ${st:-0} --streams 1,2 --rounds 3 --iters 24 ;;
+               --staging ${st:-0} --streams 1,2 --rounds ${KB_ROUNDS:-3} --iters 24 ;;
     anat)  run anat_${arg:-c4} 900 bash scripts/gpu_c4anat.sh ${TAG}_anat ;;
     sq)    IFS=: read -r c v w <<< "$arg"; n=sq_${c}_$(echo "${v:-all}${w:+_w$w}" | tr -c 'a-z0-9' '_')
            run $n 600 bash scripts/pmc.sh ${TAG}_$n "${v:-all}" $c "--windows ${w:-0}"
@@ -73,6 +74,7 @@ for step in "$@"; do
     secondary) run secondary 300 python scripts/secondary_bench.py
            run secondary_prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/secprof" -o trace -- \
                python scripts/secondary_bench.py --cpu-budget 0.2 ;;
+    hostab) run hostab 600 bash -c 'for c in c2 c4; do for st in 0 2; do python scripts/hostpath_native.py --config $c --staging $st --chunks 65536,131072,262144,524288 || exit $?; done; done' ;;
     hostpieces) run hostpieces 300 python scripts/pcap_host_pieces.py ${arg:+--pieces $arg} ;;
     host)  run host 600 bash -c 'for c in c2 c4; do python scripts/hostpath_native.py --config $c --chunks 262144 || exit $?;
                python scripts/hostpath_native.py --config $c --pageable --chunks 131072,262144 || exit $?; done' ;;

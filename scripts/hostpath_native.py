@@ -25,11 +25,14 @@ ap.add_argument("--packets", type=int, default=1 << 20)
 ap.add_argument("--chunks", default="65536,131072,262144,524288")
 ap.add_argument("--reps", type=int, default=5)
 ap.add_argument("--columns", default=None)
+ap.add_argument("--staging", type=int, default=0,
+                help="pkt_ctx_set_staging: 0 = pinned columns through the export pipeline, 2 = zero copy")
 ap.add_argument("--pageable", action="store_true",
                 help="plain numpy buffers (staged chunk pipeline) instead of pinned (zero copy)")
 args = ap.parse_args()
 
 P = pktgpu.Parser(0)
+P.set_staging(args.staging)
 n = args.packets
 if args.config == "c2":
     src, stride, offs, lens = gen.gen_c2(n).reshape(-1), 64, None, None
@@ -61,7 +64,9 @@ for ch in [int(x) for x in args.chunks.split(",")]:
         P.parse_host(slab, stride=stride, n=n, offsets=h_offs, lens=h_lens, out=out, chunk=ch)
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    print(json.dumps({"path": "pkt_parse_host " + ("(pageable: chunked copies on 3 streams)" if args.pageable else "(pinned: zero copy)"), "config": args.config,
+    print(json.dumps({"path": "pkt_parse_host " + ("(pageable: chunked copies on 3 streams)" if args.pageable else
+                                                  "(pinned: zero copy)" if args.staging == 2 else
+                                                  "(pinned: DMA in, column export kernel out)"), "config": args.config,
                       "packets": n, "chunk": ch, "ms_per_batch": round(t * 1e3, 3),
                       "gpkt_s": round(n / t / 1e9, 4), "in_GB": round(in_bytes / 1e9, 4),
                       "out_GB": round(out_bytes / 1e9, 4), "in_GB_s": round(in_bytes / t / 1e9, 2),

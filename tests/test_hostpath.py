@@ -91,9 +91,9 @@ def test_pinned_buffers(P):
 
 
 def test_pinned_indexed_zero_copy(P):
-    """Pinned slab, offsets, lens and columns: the export pipeline (chunks copied in, parsed on the
-    device, columns exported by 16-byte chunks; odd chunk sizes), and the zero-copy route (one launch
-    over the link, pkt_ctx_set_staging(2)) — the same results."""
+    """Pinned slab, offsets, lens and columns: the zero-copy route (one launch over the link); a
+    pageable slab with pinned columns: the export pipeline (chunks copied in, parsed on the device,
+    columns exported by 16-byte chunks; odd chunk sizes) — the same results."""
     buf, offs, lens = gen.gen_c4(40000, seed=11)
     h = P.host_empty(buf.shape, np.uint8)
     h[:] = buf
@@ -103,19 +103,13 @@ def test_pinned_indexed_zero_copy(P):
     hl[:] = lens
     out = {c: P.host_empty(schema.column_shape(c, len(offs)), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
     ref = oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8)
+    g = P.parse_host(h, offsets=ho, lens=hl, out=out)
+    check(g, ref, "pinned c4 zero copy")
     for chunk in (0, 4097):
         for c in out:
             out[c][...] = 0
-        g = P.parse_host(h, offsets=ho, lens=hl, out=out, chunk=chunk)
-        check(g, ref, f"pinned c4 export chunk={chunk}")
-    for c in out:
-        out[c][...] = 0
-    P.set_staging(2)
-    try:
-        g = P.parse_host(h, offsets=ho, lens=hl, out=out)
-    finally:
-        P.set_staging(0)
-    check(g, ref, "pinned c4 zero copy")
+        g = P.parse_host(buf, offsets=offs, lens=lens, out=out, chunk=chunk)
+        check(g, ref, f"pageable slab, pinned columns: export chunk={chunk}")
     # mixed: pinned slab, pageable columns -> the staged pipeline, same results
     g = P.parse_host(h, offsets=ho, lens=hl, columns="all", chunk=9999)
     check(g, oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8), "pinned slab only")
