@@ -204,6 +204,9 @@ __device__ __forceinline__ int chain_local(const uint32_t* lw, uint32_t c, uint3
 // (the second from a safe in-LDS address when the first is implausible or the chain leaves the staged
 // bytes) and the verdict is one select chain — the looped form's early returns made every
 // 64-candidate step pay exec-mask saves and restores for each hop.
+#ifndef PKTGPU_PCAP_RUNLAST
+#define PKTGPU_PCAP_RUNLAST 1  // pcapn main vs run-last: 83.5-84.2 vs 81.9-82.7 us per call (profiles/ab/r05g_pcap_guess_runlast.txt)
+#endif
 #ifndef PKTGPU_PCAP_BRANCHFREE
 #define PKTGPU_PCAP_BRANCHFREE 0  // measured: 91.3 vs 89.9 us per call with it (r04a), kept for A/B
 #endif
@@ -340,7 +343,19 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
                     : 0;
         uint64_t m = __ballot(r == 1);
         if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
+#if PKTGPU_PCAP_RUNLAST
+        // The lowest verified candidate, moved to the LAST of the run of consecutive verified
+        // candidates it starts: a record whose predecessor's payload ends in zero bytes verifies one
+        // to three bytes early too (its fields shifted by whole bytes stay plausible), and the
+        // scan's re-walk of such a wrong guess sets its critical path (pcap indexer).
+        if (m) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(m);
+            const uint64_t rest = ~(m >> f);  // bit j clear iff candidate f + j verified
+            return c0 + f + (rest ? (uint64_t)__builtin_ctzll(rest) - 1u : 63u - f);
+        }
+#else
         if (m) return c0 + (uint64_t)__builtin_ctzll(m);
+#endif
     }
     return base + kRegion;
 }
