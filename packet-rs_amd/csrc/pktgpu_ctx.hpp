@@ -45,6 +45,7 @@ struct PcapScratch {
     uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the kernel writes them)
     uint32_t epoch = 0;           // per call: block states of older calls are ignored, not cleared
     uint32_t scan_resident = 0;   // scan-kernel blocks resident at once (0 = not yet queried)
+    uint32_t guess_resident = 0;  // persistent guess-kernel blocks resident at once (0 = not yet queried)
     // a capture queued by pkt_parse_pcap_async / pkt_parse_pcap_host_async whose outcome (the words
     // above) has not been taken yet: no other index call may reuse the scratch until it is
     bool pending = false;

@@ -207,6 +207,12 @@ __device__ __forceinline__ int chain_local(const uint32_t* lw, uint32_t c, uint3
 #ifndef PKTGPU_PCAP_RUNLAST
 #define PKTGPU_PCAP_RUNLAST 1  // pcapn main vs run-last: 83.5-84.2 vs 81.9-82.7 us per call (profiles/ab/r05g_pcap_guess_runlast.txt)
 #endif
+#ifndef PKTGPU_PCAP_RUNACROSS
+#define PKTGPU_PCAP_RUNACROSS 1  // the run goes on past the step's lane 63 (0: round-5 r05g form, for A/B)
+#endif
+#ifndef PKTGPU_PCAP_DUAL
+#define PKTGPU_PCAP_DUAL 0  // measured slower: 87.9 vs 82.2 us per call (profiles/ab/r05m_pcap_lookback_spin.txt)
+#endif
 #ifndef PKTGPU_PCAP_BRANCHFREE
 #define PKTGPU_PCAP_BRANCHFREE 0  // measured: 91.3 vs 89.9 us per call with it (r04a), kept for A/B
 #endif
@@ -330,17 +336,13 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
     if (snap == 0 || snap > (1u << 30)) snap = 1u << 30;
     const uint64_t stop = len < base + kRegion ? len : base + kRegion;
     const uint32_t lim = len - lbase > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)(len - lbase);
-    for (uint64_t c0 = base; c0 < stop; c0 += 64) {
+    constexpr uint64_t kNoRun = ~0ull;
+    uint64_t run = kNoRun;  // a run of verified candidates that reached the previous step's lane 63
+    // One step of 64 candidates c0 + lane, r = chain_local's verdict for this lane's: true (and the entry
+    // in `res`) when the step decides the region's entry.
+    auto step = [&](int r, uint64_t c, uint64_t c0, uint64_t& res) -> bool {
         // The lowest candidate whose chain checks out inside the staged bytes wins; only when
         // there is none do the candidates whose chains leave them read global memory.
-        const uint64_t c = c0 + lane;
-        int r = 0;
-        if constexpr (PKTGPU_PCAP_BRANCHFREE && kMinHops == 2 && kMaxHops == 2)
-            r = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
-        else
-            r = c < stop && c + 16 <= len
-                    ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
-                    : 0;
         uint64_t m = __ballot(r == 1);
         if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
 #if PKTGPU_PCAP_RUNLAST
@@ -348,16 +350,56 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
         // candidates it starts: a record whose predecessor's payload ends in zero bytes verifies one
         // to three bytes early too (its fields shifted by whole bytes stay plausible), and the
         // scan's re-walk of such a wrong guess sets its critical path (pcap indexer).
+        // A run that reaches lane 63 goes on into the next step (the bench capture's last 7 wrong
+        // guesses were runs cut there, one byte early: profiles/ab/r05i_pcap_guess_runacross.txt).
+        if (run != kNoRun && !(m & 1u)) {
+            res = run;
+            return true;
+        }
         if (m) {
-            const uint32_t f = (uint32_t)__builtin_ctzll(m);
-            const uint64_t rest = ~(m >> f);  // bit j clear iff candidate f + j verified
-            return c0 + f + (rest ? (uint64_t)__builtin_ctzll(rest) - 1u : 63u - f);
+            const uint32_t f = run != kNoRun ? 0u : (uint32_t)__builtin_ctzll(m);
+            const uint64_t rest = ~(m >> f);  // bit j clear iff candidate f + j verified (j < 64 - f)
+            const uint32_t rl = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;  // the run's length
+            if (f + rl < 64u || !PKTGPU_PCAP_RUNACROSS) {
+                res = c0 + f + rl - 1u;
+                return true;
+            }
+            run = c0 + 63;
         }
 #else
-        if (m) return c0 + (uint64_t)__builtin_ctzll(m);
+        if (m) {
+            res = c0 + (uint64_t)__builtin_ctzll(m);
+            return true;
+        }
 #endif
+        return false;
+    };
+    uint64_t res = 0;
+    if constexpr (PKTGPU_PCAP_DUAL && kMinHops == 2 && kMaxHops == 2) {
+        // two steps' candidates per lane checked together (two independent branch-free chains: their
+        // LDS reads overlap), then decided in step order
+        for (uint64_t c0 = base; c0 < stop; c0 += 128) {
+            const uint64_t ca = c0 + lane, cb = ca + 64;
+            const int ra = ca < stop && ca + 16 <= len ? chain_local2(lw, (uint32_t)(ca - lbase), STAGED, lim, snap) : 0;
+            const int rb = cb < stop && cb + 16 <= len ? chain_local2(lw, (uint32_t)(cb - lbase), STAGED, lim, snap) : 0;
+            if (step(ra, ca, c0, res)) return res;
+            if (c0 + 64 >= stop) break;
+            if (step(rb, cb, c0 + 64, res)) return res;
+        }
+    } else {
+        for (uint64_t c0 = base; c0 < stop; c0 += 64) {
+            const uint64_t c = c0 + lane;
+            int r = 0;
+            if constexpr (PKTGPU_PCAP_BRANCHFREE && kMinHops == 2 && kMaxHops == 2)
+                r = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
+            else
+                r = c < stop && c + 16 <= len
+                        ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
+                        : 0;
+            if (step(r, c, c0, res)) return res;
+        }
     }
-    return base + kRegion;
+    return run != kNoRun ? run : base + kRegion;
 }
 
 // Tile states cross XCDs (each XCD has its own L2): every access is a device-scope relaxed atomic
@@ -471,6 +513,26 @@ __device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, u
 #ifndef PKTGPU_PCAP_LANEWALK
 #define PKTGPU_PCAP_LANEWALK 1
 #endif
+#ifndef PKTGPU_PCAP_PERSIST
+#define PKTGPU_PCAP_PERSIST 0  // measured slower in every form: profiles/ab/r05o_pcap_guess_persistent.txt
+#endif
+// Issue priority of wave 0 while it walks the block's four regions (s_setprio; 0 = unchanged): the
+// other three waves of the block wait for the walks at the barrier, so a walk's hops should not queue
+// behind other blocks' candidate scans on the SIMD.
+#ifndef PKTGPU_PCAP_WALKPRIO
+#define PKTGPU_PCAP_WALKPRIO 0  // no effect measured (profiles/ab/r05p_pcap_walk_prio.txt)
+#endif
+#ifndef PKTGPU_PCAP_PREFETCH
+#define PKTGPU_PCAP_PREFETCH 1
+#endif
+#ifndef PKTGPU_PCAP_WPE
+#define PKTGPU_PCAP_WPE 0
+#endif
+#if PKTGPU_PCAP_WPE
+#define PCAP_PERSIST_WPE __attribute__((amdgpu_waves_per_eu(PKTGPU_PCAP_WPE, PKTGPU_PCAP_WPE)))
+#else
+#define PCAP_PERSIST_WPE
+#endif
 // Diagnostic build only (-DPKTGPU_STAMPS=1, read by scripts/pcap_stamps.py): per wave of the guess
 // kernel, s_memrealtime at the start, after the staging barrier, after its candidate scan, after the
 // walk barrier and after its stores drained, + XCC id and the entry's distance from the region
@@ -520,6 +582,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         PCAP_STAMP(2);
         if (lane == 0) s_entry[w] = entry;
         __syncthreads();
+        if (PKTGPU_PCAP_WALKPRIO && w == 0) __builtin_amdgcn_s_setprio(PKTGPU_PCAP_WALKPRIO);
         if (w == 0 && lane < (uint32_t)kWaves) {
             const uint32_t kk = blockIdx.x * kWaves + lane;
             const uint64_t en = s_entry[lane];
@@ -534,6 +597,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             s_exit[lane] = ex;
             s_cnt[lane] = cw;
         }
+        if (PKTGPU_PCAP_WALKPRIO && w == 0) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         PCAP_STAMP(3);
         if (k >= K) return;
@@ -592,6 +656,78 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
             const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
             __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             S.dev[1] = mg;
+        }
+    }
+}
+
+// GUESS, persistent form (PKTGPU_PCAP_PERSIST): a grid the device holds at once, each block taking
+// tiles blockIdx.x, + gridDim.x, ... and loading its NEXT tile's 16 KiB into registers while it scans and
+// walks the current one, so a tile's memory latency (the one-shot kernel's staging: 1.64 us median,
+// p90 3.9 us of a 7 us wave, profiles/pcap/r05k_stamps.txt) hides behind the previous tile's LDS work;
+// the same per-tile work as pcap_guess_kernel's lane-walk path (files below 2 GiB: lane_walk2).
+constexpr uint32_t kGuessStaged = kWaves * kRegion;
+constexpr uint32_t kStagePieces = kGuessStaged / 16 + 2, kStagePer = (kStagePieces + 255) / 256;
+__device__ __forceinline__ void stage_load(uint4 (&v)[kStagePer], const uint8_t* buf, uint64_t base, uint64_t len,
+                                           uint32_t t) {
+#pragma unroll
+    for (uint32_t i = 0; i < kStagePer; i++) {
+        const uint32_t q = t + i * 256u;
+        const uint64_t a = base + 16ull * q;
+        v[i] = make_uint4(0, 0, 0, 0);
+        if (q <= kGuessStaged / 16 && a < len) v[i] = *reinterpret_cast<const uint4*>(buf + a);
+    }
+}
+__global__ __launch_bounds__(256) PCAP_PERSIST_WPE void pcap_guess_persist_kernel(const uint8_t* __restrict__ buf, uint64_t len,
+                                                                 uint32_t K, uint32_t ntiles, Scratch S) {
+    __shared__ uint4 lds[kStagePieces];
+    __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
+    __shared__ uint64_t s_entry[kWaves], s_exit[kWaves];
+    __shared__ uint32_t s_cnt[kWaves];
+    const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
+    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
+    uint4 v[kStagePer];
+    uint32_t tile = blockIdx.x;
+    if (PKTGPU_PCAP_PREFETCH && tile < ntiles) stage_load(v, buf, (uint64_t)tile * kGuessStaged, len, t);
+    for (; tile < ntiles; tile += gridDim.x) {
+        const uint64_t lbase = (uint64_t)tile * kGuessStaged;
+        if (!PKTGPU_PCAP_PREFETCH) stage_load(v, buf, lbase, len, t);
+        __syncthreads();  // the previous tile's LDS reads are done
+#pragma unroll
+        for (uint32_t i = 0; i < kStagePer; i++)
+            if (t + i * 256u < kStagePieces) lds[t + i * 256u] = v[i];
+        __syncthreads();
+        // the next tile's bytes in flight while this one is scanned and walked
+        if (PKTGPU_PCAP_PREFETCH && tile + gridDim.x < ntiles)
+            stage_load(v, buf, (uint64_t)(tile + gridDim.x) * kGuessStaged, len, t);
+        const uint32_t k = tile * kWaves + w;
+        const uint64_t base = (uint64_t)k * kRegion;
+        const uint64_t entry = k >= K ? base + kRegion : (k == 0 ? 24 : guess_entry<kGuessStaged>(buf, len, lw, lbase, k));
+        if (lane == 0) s_entry[w] = entry;
+        __syncthreads();
+        if (w == 0 && lane < (uint32_t)kWaves) {
+            const uint32_t kk = tile * kWaves + lane;
+            uint64_t ex = 0;
+            uint32_t cw = 0;
+            lane_walk2(lw, lbase, lst[lane], (uint64_t)kk * kRegion, s_entry[lane], len, kk < K, ex, cw);
+            if (S.partial) cw &= kCntMask;
+            s_exit[lane] = ex;
+            s_cnt[lane] = cw;
+        }
+        __syncthreads();
+        if (k < K) {
+            const uint32_t cw = s_cnt[w], cnt = cw & kCntMask;
+            uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
+            for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
+            if (lane == 0) {
+                S.rentry[k] = entry;
+                S.rexit[k] = s_exit[w];
+                S.rcnt[k] = cw;
+                if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
+                    const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
+                    __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    S.dev[1] = mg;
+                }
+            }
         }
     }
 }
@@ -724,9 +860,21 @@ __device__ __forceinline__ bool seam_bad(const Agg& pre, const Agg& r) {
 #ifndef PKTGPU_PCAP_REUSE
 #define PKTGPU_PCAP_REUSE 1
 #endif
+// The scan blocks write the records after their look-back (no emit kernel).
+#ifndef PKTGPU_PCAP_SCANEMIT
+#define PKTGPU_PCAP_SCANEMIT 0  // measured slower: 82.1 vs 76.6 us per call (profiles/ab/r05q_pcap_scan_emit.txt)
+#endif
+#ifndef PKTGPU_PCAP_AGG0
+#define PKTGPU_PCAP_AGG0 1
+#endif
+#ifndef PKTGPU_PCAP_SPIN
+#define PKTGPU_PCAP_SPIN 1  // 78.1 vs 81.8-82.6 us per call (profiles/ab/r05m_pcap_lookback_spin.txt)
+#endif
+constexpr uint32_t kSpinMax = 4096;  // then the block-wide retry
 // Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
 __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
-                                                        uint32_t nb, int ticket, Scratch S) {
+                                                        uint32_t nb, int ticket, Scratch S, uint64_t cap,
+                                                        uint64_t* __restrict__ offsets, uint32_t* __restrict__ lens) {
     __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
     __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
     __shared__ uint64_t sen[kScanRegions], sex[kScanRegions];
@@ -878,7 +1026,9 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             uint32_t st = 0;  // 0 unpublished, 1 aggregate, 2 exact
             Agg a = agg_identity();
             uint64_t xl = 0, xc = 0, xm = 0;
-            if (jj >= 0) {
+            // (PKTGPU_PCAP_SPIN: a lane whose block has published nothing yet re-reads it after a short
+            // sleep, up to kSpinMax times, instead of the whole window being re-read after a block-wide retry)
+            for (uint32_t spin = 0; jj >= 0; spin++) {
                 // all seven fields in one round trip; a state counts only with the epoch in every field
                 const BlkDesc* d = S.blk + jj;
                 const uint64_t il_ = ld_agent(&d->i_last), ic_ = ld_agent(&d->i_cnt), ib_ = ld_agent(&d->i_bits);
@@ -893,7 +1043,19 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                 } else if (tag_of(af) == ep && tag_of(al) == ep && tag_of(ac) == ep && tag_of(ab) == ep) {
                     st = 1;
                     a = Agg{af & kValMask, al & kValMask, ac & kValMask, (uint32_t)(ab & 15u)};
+                    // block 0's consistent aggregate IS its exact state (region 0 starts at 24 by
+                    // definition; block 0 has no seam before it to fix): no wait for its exact
+                    // state's publication, which a look-back's first read usually missed
+                    // (one retry per block, ~2.5 us: profiles/pcap/r05k_stamps.txt)
+                    if (PKTGPU_PCAP_AGG0 && jj == 0 && !(a.bits & (kBitNone | kBitBad)) && a.first == 24) {
+                        st = 2;
+                        xl = a.last;
+                        xc = a.cnt;
+                        xm = a.bits & kBitErr;
+                    }
                 }
+                if (st || !PKTGPU_PCAP_SPIN || spin >= kSpinMax) break;
+                __builtin_amdgcn_s_sleep(1);
             }
             // the nearest exact block in the window (the smallest thread index with st == 2)
             if (t == 0) s_near = 256;
@@ -1018,7 +1180,34 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     }
     // each region's exact record prefix (the emit kernel writes the records): the records of the
     // regions before it in the block are the exclusive composition's count
-    if (PKTGPU_PCAP_REUSE) {
+    if (PKTGPU_PCAP_SCANEMIT && PKTGPU_PCAP_REUSE) {
+        // the records themselves (no emit kernel): thread t writes region t's, from its list read 8
+        // entries (16 B) at a time — the next record's offset ends each one's incl_len, the region's
+        // exit ends its last (a prefix of a capture: the last one's header, as pcap_emit_kernel)
+        const uint32_t cnt = k < K ? (scw[t] & kCntMask) : 0u;
+        const uint64_t first = c_before + pre_cur.cnt, rbase = (uint64_t)k * kRegion, ex = sex[t];
+        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
+        for (uint32_t j0 = 0; j0 < cnt && first + j0 < cap; j0 += 8) {
+            const uint4 q = *reinterpret_cast<const uint4*>(list + j0);
+            const uint32_t nx = j0 + 8 < cnt ? list[j0 + 8] : 0u;
+            const uint32_t e[9] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu, q.z >> 16,
+                                   q.w & 0xFFFFu, q.w >> 16, nx};
+#pragma unroll
+            for (uint32_t u = 0; u < 8; u++) {
+                const uint32_t j = j0 + u;
+                if (j >= cnt || first + j >= cap) break;
+                const uint64_t pos = rbase + e[u];
+                const uint64_t next = j + 1 < cnt ? rbase + e[u + 1] : ex;
+                uint32_t incl = (uint32_t)(next - pos - 16);
+                if (S.partial && j + 1 == cnt) {
+                    const uint8_t* h = buf + pos + 8;
+                    incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+                }
+                offsets[first + j] = pos + 16;
+                lens[first + j] = incl;
+            }
+        }
+    } else if (PKTGPU_PCAP_REUSE) {
         if (k < K) S.rpre[k] = c_before + pre_cur.cnt;
     } else {
         uint32_t x = k < K ? (scw[t] & kCntMask) : 0u, c = x;
@@ -1192,7 +1381,20 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
-    hipLaunchKernelGGL(pcap_guess_kernel, dim3((K + kWaves - 1) / kWaves), blk, 0, s, buf, len, K, S);
+    const uint32_t ntiles = (K + kWaves - 1) / kWaves;
+    if (PKTGPU_PCAP_PERSIST && !PKTGPU_STAMPS && len <= 0x7FFFFFF0ull) {
+        if (!pc.guess_resident) {  // guess blocks the device holds at once
+            int per_cu = 0, cus = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_guess_persist_kernel, 256, 0) != hipSuccess ||
+                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
+                per_cu = cus = 0;
+            pc.guess_resident = (uint32_t)std::max(1, per_cu * cus);
+        }
+        hipLaunchKernelGGL(pcap_guess_persist_kernel, dim3(std::min(ntiles, pc.guess_resident)), blk, 0, s, buf, len, K,
+                           ntiles, S);
+    } else {
+        hipLaunchKernelGGL(pcap_guess_kernel, dim3(ntiles), blk, 0, s, buf, len, K, S);
+    }
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     if (!pc.scan_resident) {  // scan blocks the device holds at once
         int per_cu = 0, cus = 0;
@@ -1207,12 +1409,13 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // such block has been dispatched (is resident or finished) — whatever else occupies the device,
     // e.g. the other ctx's capture of the async entries.  The occupancy test keeps the ticket for a
     // grid the device could not hold at once even alone.
-    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S);
+    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S, cap,
+                       offsets, lens);
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
-    if (cap) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens, buf);
+    if (cap && !PKTGPU_PCAP_SCANEMIT) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens, buf);
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");

@@ -49,6 +49,15 @@ assert cnt.value == n and np.array_equal(o.cpu().numpy(), offs)
 xa = st.cpu().numpy().view(np.int64)
 y = xa[K * 8:].reshape(NB, 16).copy()
 x = xa[:K * 8].reshape(K, 8)
+# wrong guesses: regions whose guessed entry is not the first record start at or past the region base
+st_ = offs.astype(np.int64) - 16
+bases = np.arange(K, dtype=np.int64) * 4096
+i_ = np.searchsorted(st_, bases)
+true_ = np.where((i_ < len(st_)) & (st_[np.minimum(i_, len(st_) - 1)] < bases + 4096),
+                 st_[np.minimum(i_, len(st_) - 1)] - bases, 4096)
+bad_ = np.nonzero((x[:, 0] != 0) & (x[:, 6] != true_))[0]
+print(f"wrong guesses: {len(bad_)}" + "".join(f"\n  region {k} (k % 4 = {k % 4}): guess {x[k, 6]} true {true_[k]}"
+                                                for k in bad_[:16]))
 x = x[x[:, 0] != 0].copy()
 t00 = x[:, 0].min()
 x[:, :5] -= t00  # one device-wide constant clock
@@ -87,5 +96,6 @@ for k, v in ss.items():
     print(f"  {k:28s} median {np.median(v) / f:7.2f} us  p90 {np.percentile(v, 90) / f:7.2f} us  max {v.max() / f:7.2f} us")
 print(f"  blocks with fixes: {(y[:, 5] > 0).sum()} (regions re-walked {y[:, 5].sum()}); look-back retries "
       f"median {np.median(y[:, 6] & 0xFFFF):.0f} max {(y[:, 6] & 0xFFFF).max()}; first-seam waits max {(y[:, 6] >> 16).max()}")
+print("  scan blocks with fixes:", " ".join(str(int(b)) for b in np.nonzero(y[:, 5] > 0)[0][:16]))
 o_ = np.argsort(y[:, 0])
 print("  look-back done (us) by start:", " ".join(f"{v / f:.1f}" for v in y[o_, 3][:: max(1, len(y) // 16)]))

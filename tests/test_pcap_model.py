@@ -69,25 +69,29 @@ TILE = 4  # regions per guess block (staged together, pcap_guess_kernel)
 def guess(b, k, snap):
     """First candidate of the region, 64 offsets per step: the lowest whose chain checks out in
     the tile's staged bytes (TILE regions + 16 B), else the lowest that checks out with reads past
-    them, moved to the last of the run of consecutive verified candidates it starts (PKTGPU_PCAP_RUNLAST);
+    them, moved to the last of the run of consecutive verified candidates it starts, across steps
+    (PKTGPU_PCAP_RUNLAST);
     none in the region -> "no record starts here"."""
     base = k * R
     stop = min(len(b), base + R)
     lend = (k // TILE + 1) * TILE * R
-    def run_last(ok):  # the last of the run of consecutive verified candidates the lowest one starts
-        c = min(ok)
-        while c + 1 in ok:
-            c += 1
-        return c
+    run = None  # a run of verified candidates that reached the previous step's last lane
     for c0 in range(base, stop, 64):
         cs = [c for c in range(c0, min(c0 + 64, stop)) if c + 16 <= len(b)]
         rs = [chain_ok(b, c, stop, snap, lend) for c in cs]
         ok = {c for c, r in zip(cs, rs) if r == 1}
         if not ok:
             ok = {c for c, r in zip(cs, rs) if r == 2 and chain_ok(b, c, stop, snap) == 1}
-        if ok:
-            return run_last(ok)
-    return base + R
+        if run is not None and c0 not in ok:
+            return run
+        if ok:  # the last of the run of consecutive verified candidates (from the lowest, or continued)
+            c = c0 if run is not None else min(ok)
+            while c + 1 in ok:
+                c += 1
+            if c < c0 + 63:
+                return c
+            run = c
+    return run if run is not None else base + R
 
 
 B = 256  # regions per scan block (pcap_scan_kernel)
