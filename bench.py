@@ -476,8 +476,8 @@ def pcap_record(P, torch, dev, n=1 << 20, reps=10):
     finally:
         P2.close()
     return {"workload": f"C4 capture: {n} records of the 22 reference templates, {buf.size} B pcap file in HBM",
-            "step": "pkt_parse_pcap: pcap_guess_kernel + pcap_scan_kernel (record boundaries, written by the "
-                    "scan) + parse_kernel (all columns, record count read on the device); one blocking call",
+            "step": "pkt_parse_pcap: pcap_guess_kernel + pcap_scan_kernel + pcap_emit_kernel (record boundaries, exact; written by the emit "
+                    "kernel) + parse_kernel (all columns, record count read on the device); one blocking call",
             "ms_per_step": round(t * 1e3, 4), "Grecords/s": round(n / t / 1e9, 4),
             "file_GB/s": round(buf.size / t / 1e9, 2), "index_matches_host_indexer": bool(ok),
             "reps": reps, "timing": "wall clock per step, median", "index": index,

@@ -79,6 +79,12 @@ constexpr uint32_t kCntErr = 0x80000000u, kCntMask = 0x7FFFFFFFu;
 
 constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
 constexpr uint32_t kEmitRegions = 16;   // regions per emit block
+#ifndef PKTGPU_PCAP_EMITR
+#define PKTGPU_PCAP_EMITR 32  // 0: pcap_emit_kernel; 75.3-75.8 vs 76.5-76.6 us per call (profiles/ab/r05s_pcap_emit_wide.txt)
+#endif
+#ifndef PKTGPU_PCAP_EMITPER
+#define PKTGPU_PCAP_EMITPER 4
+#endif
 
 struct Scratch {
     uint64_t* rentry;  // per region: the walk's entry (>= the region's end: no record starts in it)
@@ -1288,6 +1294,76 @@ __global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap
     }
 }
 
+// Emit, wider blocks (PKTGPU_PCAP_EMITR = NR regions per block, NR <= 64): every thread takes up to
+// PER records per pass and issues all their list loads before the first store, so a block waits one
+// round trip for its region words and one for its lists instead of one per record step.
+template <uint32_t NR, uint32_t PER>
+__global__ __launch_bounds__(256) void pcap_emit_wide_kernel(uint32_t K, uint64_t cap, Scratch S,
+                                                             uint64_t* __restrict__ offsets,
+                                                             uint32_t* __restrict__ lens, const uint8_t* __restrict__ buf) {
+    static_assert(NR >= 2 && NR <= 64 && (NR & (NR - 1)) == 0, "NR: a power of two <= 64");
+    __shared__ uint32_t cpre[NR + 1];
+    __shared__ uint64_t cex[NR];
+    const uint32_t k0 = blockIdx.x * NR, t = threadIdx.x;
+    const uint64_t first = S.rpre[k0];
+    if (t < 64) {
+        const bool in = t < NR && k0 + t < K;
+        const uint32_t c = in ? (S.rcnt[k0 + t] & kCntMask) : 0;
+        if (t < NR) cex[t] = in ? S.rexit[k0 + t] : 0;
+        uint32_t x = c;
+#pragma unroll
+        for (uint32_t d = 1; d < NR; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (t >= d) x += y;
+        }
+        if (t < NR) cpre[t] = x - c;
+        if (t == NR - 1) cpre[NR] = x;
+    }
+    __syncthreads();
+    const uint32_t total = cpre[NR];
+    for (uint32_t i0 = 0; i0 < total && first + i0 < cap; i0 += 256u * PER) {
+        uint32_t rr[PER], li[PER], cc[PER], a[PER], b[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            uint32_t r = 0;
+#pragma unroll
+            for (uint32_t bb = NR / 2; bb; bb >>= 1)
+                if (cpre[r + bb] <= i) r += bb;
+            rr[u] = r;
+            li[u] = i - cpre[r];
+            cc[u] = cpre[r + 1] - cpre[r];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            a[u] = b[u] = 0;
+            if (i < total) {
+                const uint16_t* list = S.list + (uint64_t)(k0 + rr[u]) * kMaxRec;
+                a[u] = list[li[u]];
+                if (li[u] + 1 < cc[u]) b[u] = list[li[u] + 1];
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            const uint64_t idx = first + i;
+            if (i >= total || idx >= cap) continue;
+            const uint64_t base = (uint64_t)(k0 + rr[u]) * kRegion;
+            const uint64_t pos = base + a[u];
+            const bool last = li[u] + 1 == cc[u];
+            const uint64_t next = last ? cex[rr[u]] : base + b[u];
+            uint32_t incl = (uint32_t)(next - pos - 16);
+            if (S.partial && last) {  // a prefix of a capture: as pcap_emit_kernel
+                const uint8_t* h = buf + pos + 8;
+                incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+            }
+            offsets[idx] = pos + 16;
+            lens[idx] = incl;
+        }
+    }
+}
+
 
 }  // namespace
 
@@ -1415,7 +1491,14 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
-    if (cap && !PKTGPU_PCAP_SCANEMIT) hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S, offsets, lens, buf);
+    if (cap && !PKTGPU_PCAP_SCANEMIT) {
+        if constexpr (PKTGPU_PCAP_EMITR != 0)
+            hipLaunchKernelGGL((pcap_emit_wide_kernel<PKTGPU_PCAP_EMITR, PKTGPU_PCAP_EMITPER>),
+                               dim3((K + PKTGPU_PCAP_EMITR - 1) / PKTGPU_PCAP_EMITR), blk, 0, s, K, cap, S, offsets, lens, buf);
+        else
+            hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S,
+                               offsets, lens, buf);
+    }
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
