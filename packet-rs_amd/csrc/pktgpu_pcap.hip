@@ -877,6 +877,115 @@ __device__ __forceinline__ bool seam_bad(const Agg& pre, const Agg& r) {
 #define PKTGPU_PCAP_SPIN 1  // 78.1 vs 81.8-82.6 us per call (profiles/ab/r05m_pcap_lookback_spin.txt)
 #endif
 constexpr uint32_t kSpinMax = 4096;  // then the block-wide retry
+// The records, written by blocks of the scan kernel's own grid (PKTGPU_PCAP_COEMIT): blocks past the nb
+// scan blocks each take NR regions and wait — a relaxed agent-scope load per region, a short sleep between
+// tries — for the region words the scan blocks publish once their look-back is done: (record prefix << 1
+// | fixed), tagged with the call's epoch.  Then the wide emit over them (16-byte list loads issued before
+// the stores).  The records of a region its scan block re-walked are written by that block itself (their
+// list and exit were written in this kernel, by another CU); every other region's list, count and exit come
+// from the guess kernel, visible across the launch boundary.  Progress: the scan blocks have lower blockIdx,
+// so all of them are dispatched before any emit block, and none waits for an emit block.  This takes the
+// emit kernel's launch boundary off the call and overlaps its start with the scan (profiles/ab/r05v_*).
+#ifndef PKTGPU_PCAP_COEMIT
+#define PKTGPU_PCAP_COEMIT 0  // 0.3-0.9 us per call: not adopted (profiles/ab/r05v_pcap_coemit.txt)
+#endif
+constexpr uint32_t kCoEmitRegions = 64;
+#ifndef PKTGPU_PCAP_COEMIT_SLEEP
+#define PKTGPU_PCAP_COEMIT_SLEEP 12
+#endif
+constexpr uint32_t kCoEmitSpin = 1u << 22;
+__device__ __forceinline__ void coemit_block(uint32_t eb, uint32_t K, uint64_t cap, const Scratch& S,
+                                             uint64_t* __restrict__ offsets, uint32_t* __restrict__ lens,
+                                             const uint8_t* __restrict__ buf) {
+    constexpr uint32_t NR = kCoEmitRegions, PER = 4;
+    __shared__ uint64_t e_pre[NR + 1], e_ex[NR];
+    __shared__ uint32_t e_cpre[NR + 1], e_lastc;
+    __shared__ uint8_t e_fx[NR + 1];
+    const uint32_t t = threadIdx.x, k0 = eb * NR;
+    if (k0 >= K) return;
+    // one lane polls the last word the block needs (a scan block publishes its regions' words
+    // together), sleeping ~0.3 us between tries: 745 blocks x 65 polling lanes loaded the look-back's
+    // device-scope reads (profiles/ab/r05v_pcap_coemit.txt)
+    if (t == 0) {
+        const uint32_t kp = k0 + NR < K ? k0 + NR : K - 1;
+        for (uint32_t sp = 0; sp < kCoEmitSpin && tag_of(ld_agent(&S.rpre[kp])) != S.epoch; sp++)
+            __builtin_amdgcn_s_sleep(PKTGPU_PCAP_COEMIT_SLEEP);
+    }
+    __syncthreads();
+    if (t <= NR) {
+        const uint32_t k = k0 + t;
+        uint64_t pre = 0;
+        uint32_t fx = 0;
+        if (k < K) {
+            uint64_t pw = 0;
+            bool have = false;
+            for (uint32_t sp = 0;; sp++) {
+                pw = ld_agent(&S.rpre[k]);
+                if (tag_of(pw) == S.epoch) {
+                    have = true;
+                    break;
+                }
+                if (sp >= kCoEmitSpin) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!have)  // never expected: the call then reports an error instead of hanging
+                __hip_atomic_store(&S.host[kHostErr], (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            pre = (pw & kValMask) >> 1;
+            fx = (uint32_t)(pw & 1u);
+            if (t < NR) e_ex[t] = S.rexit[k];
+            if (k == K - 1) e_lastc = fx ? 0u : (S.rcnt[k] & kCntMask);
+        }
+        e_pre[t] = pre;
+        e_fx[t] = (uint8_t)fx;
+    }
+    __syncthreads();
+    const uint64_t p0 = e_pre[0];
+    const uint64_t total = k0 + NR < K ? e_pre[NR] - p0 : e_pre[K - 1 - k0] + e_lastc - p0;
+    if (t <= NR) e_cpre[t] = k0 + t < K ? (uint32_t)(e_pre[t] - p0) : (uint32_t)total;
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < total && p0 + i0 < cap; i0 += 256u * PER) {
+        uint32_t rr[PER], li[PER], cc[PER], a[PER], b[PER];
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            uint32_t r = 0;
+#pragma unroll
+            for (uint32_t bb = NR / 2; bb; bb >>= 1)
+                if (e_cpre[r + bb] <= i) r += bb;
+            rr[u] = r;
+            li[u] = i - e_cpre[r];
+            cc[u] = e_cpre[r + 1] - e_cpre[r];
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            a[u] = b[u] = 0;
+            if (i < total && !e_fx[rr[u]]) {
+                const uint16_t* list = S.list + (uint64_t)(k0 + rr[u]) * kMaxRec;
+                a[u] = list[li[u]];
+                if (li[u] + 1 < cc[u]) b[u] = list[li[u] + 1];
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < PER; u++) {
+            const uint32_t i = i0 + u * 256u + t;
+            const uint64_t idx = p0 + i;
+            if (i >= total || idx >= cap || e_fx[rr[u]]) continue;
+            const uint64_t base = (uint64_t)(k0 + rr[u]) * kRegion;
+            const uint64_t pos = base + a[u];
+            const bool last = li[u] + 1 == cc[u];
+            const uint64_t next = last ? e_ex[rr[u]] : base + b[u];
+            uint32_t incl = (uint32_t)(next - pos - 16);
+            if (S.partial && last) {  // a prefix of a capture: as pcap_emit_kernel
+                const uint8_t* h = buf + pos + 8;
+                incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+            }
+            offsets[idx] = pos + 16;
+            lens[idx] = incl;
+        }
+    }
+}
+
 // Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
 __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                         uint32_t nb, int ticket, Scratch S, uint64_t cap,
@@ -888,6 +997,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     __shared__ uint32_t fq[kScanRegions];
     __shared__ uint64_t fe[kScanRegions];
     __shared__ uint8_t sbad[kScanRegions];
+    __shared__ uint8_t sfix[kScanRegions];  // re-walked in this kernel (PKTGPU_PCAP_COEMIT)
     __shared__ Agg wtot[kWaves];
     __shared__ int32_t widx[kWaves];
     __shared__ uint32_t s_blk, s_nf, s_retry, s_near, csum[kWaves];
@@ -899,6 +1009,10 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     uint64_t t_bx = 0;  // after the first block composition
     uint64_t bx[2] = {0, 0};
 #endif
+    if (PKTGPU_PCAP_COEMIT && blockIdx.x >= nb) {  // an emit block (uniform)
+        coemit_block(blockIdx.x - nb, K, cap, S, offsets, lens, buf);
+        return;
+    }
     PCAP_STAMP(0);
     // the block order: blockIdx when the device could hold the whole grid at once (the host checks
     // the occupancy; progress then rests on the dispatcher launching workgroups in blockIdx order, so
@@ -908,6 +1022,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     __syncthreads();
     const uint32_t blk = s_blk;
     const uint32_t k = blk * kScanRegions + t;
+    sfix[t] = 0;
     if (k < K) {
         sen[t] = S.rentry[k];
         sex[t] = S.rexit[k];
@@ -945,6 +1060,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                 for (uint32_t j = lane; j < cnt; j += 64) dst[j] = lst[w][j];
                 if (lane == 0) {
                     sen[r] = e;
+                    sfix[r] = 1;
                     sex[r] = ex;
                     scw[r] = cw;
                     S.rentry[kk] = e;
@@ -964,6 +1080,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             if (lane == 0) {
                 const uint32_t cw = cnt | (err ? kCntErr : 0u);
                 sen[r] = e;
+                sfix[r] = 1;
                 sex[r] = exit;
                 scw[r] = cw;
                 S.rentry[kk] = e;
@@ -1212,6 +1329,28 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                 offsets[first + j] = pos + 16;
                 lens[first + j] = incl;
             }
+        }
+    } else if (PKTGPU_PCAP_COEMIT && PKTGPU_PCAP_REUSE) {
+        if (k < K) {
+            const uint64_t first = c_before + pre_cur.cnt;
+            const bool fx = sfix[t] != 0;
+            if (fx && cap) {  // a region this block re-walked: its records from here (see coemit_block)
+                const uint32_t cnt = scw[t] & kCntMask;
+                const uint64_t rbase = (uint64_t)k * kRegion, ex = sex[t];
+                const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
+                for (uint32_t j = 0; j < cnt && first + j < cap; j++) {
+                    const uint64_t pos = rbase + list[j];
+                    const uint64_t next = j + 1 < cnt ? rbase + list[j + 1] : ex;
+                    uint32_t incl = (uint32_t)(next - pos - 16);
+                    if (S.partial && j + 1 == cnt) {
+                        const uint8_t* h = buf + pos + 8;
+                        incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+                    }
+                    offsets[first + j] = pos + 16;
+                    lens[first + j] = incl;
+                }
+            }
+            st_agent(&S.rpre[k], tagged(S.epoch, (first << 1) | (fx ? 1u : 0u)));
         }
     } else if (PKTGPU_PCAP_REUSE) {
         if (k < K) S.rpre[k] = c_before + pre_cur.cnt;
@@ -1485,13 +1624,14 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // such block has been dispatched (is resident or finished) — whatever else occupies the device,
     // e.g. the other ctx's capture of the async entries.  The occupancy test keeps the ticket for a
     // grid the device could not hold at once even alone.
-    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S, cap,
-                       offsets, lens);
+    const uint32_t ne = (PKTGPU_PCAP_COEMIT && cap) ? (K + kCoEmitRegions - 1) / kCoEmitRegions : 0u;
+    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb + ne), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S,
+                       cap, offsets, lens);
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
-    if (cap && !PKTGPU_PCAP_SCANEMIT) {
+    if (cap && !PKTGPU_PCAP_SCANEMIT && !PKTGPU_PCAP_COEMIT) {
         if constexpr (PKTGPU_PCAP_EMITR != 0)
             hipLaunchKernelGGL((pcap_emit_wide_kernel<PKTGPU_PCAP_EMITR, PKTGPU_PCAP_EMITPER>),
                                dim3((K + PKTGPU_PCAP_EMITR - 1) / PKTGPU_PCAP_EMITR), blk, 0, s, K, cap, S, offsets, lens, buf);
