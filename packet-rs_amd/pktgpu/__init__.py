@@ -213,14 +213,15 @@ class Parser:
         """pkt_parse_pcap: a pcap file in the uint8 device tensor `buf` -> (n records, {column: device
         tensor} sized for cap records (slot columns [16][cap]), offsets, lens), index and parse in one
         call with one host synchronisation.  cap=None: the file's size bounds the count (>= 16 B per
-        record), which sizes the outputs."""
+        record), which sizes the outputs.  `out` may also be a PktOut built once by out_struct() (it is
+        then returned in place of the dict): the 49 column pointers are not marshalled per call."""
         torch = _torch()
         assert buf.dtype == torch.uint8 and buf.is_cuda and buf.is_contiguous()
         e = ENTRY_ID[entry] if isinstance(entry, str) else int(entry)
         if cap is None:
             cap = max(1, (buf.numel() - 24) // 16)
         res = out if out is not None else self.alloc(cap, columns)
-        o = self.out_struct(res)
+        o = res if isinstance(res, self._lib.PktOut) else self.out_struct(res)
         offsets = offsets if offsets is not None else torch.empty(cap, dtype=torch.uint64, device=self.torch_device)
         lens = lens if lens is not None else torch.empty(cap, dtype=torch.uint32, device=self.torch_device)
         n = ctypes.c_uint64()
