@@ -255,6 +255,13 @@ def test_parse_pcap_fused_vs_oracle(P):
         else:
             assert np.array_equal(gv[:n], ov), k
             assert (gv[n:].view(np.uint8) == 0xEE).all(), k  # past the count: untouched
+    # the same call through an output descriptor built once (out_struct: what bench.py's pcap step
+    # passes), into fresh columns: the same columns
+    res2 = P.alloc(cap, "all")
+    m2, g2, _, _ = P.parse_pcap(dev(buf), cap, out=P.out_struct(res2))
+    assert m2 == n and isinstance(g2, P._lib.PktOut)
+    for k in ("status", "n_hdrs", "payload_off", "hdr_mask", "ipv4_src", "udp_dst"):
+        assert np.array_equal(res2[k][:n].cpu().numpy(), g[k][:n].cpu().numpy()), k
     m, g, o, l = P.parse_pcap(dev(buf), 1000, columns=["chain"])
     assert m == n and np.array_equal(o.cpu().numpy(), offs[:1000])
     ref = oracle.parse_batch(buf, 1000, offsets=offs[:1000], lens=lens[:1000], columns=list(g), nthreads=8)
