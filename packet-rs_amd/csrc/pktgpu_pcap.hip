@@ -30,8 +30,9 @@
 //            publishes its exact state and writes each region's exact record prefix.  The last
 //            block writes the total and the error flag to pinned host words and the parse's count
 //            to a device word.
-//   EMIT (pcap_emit_kernel)  16 regions per block, one record per thread: offset = pos + 16,
-//            incl_len = next pos - pos - 16 (the last one from the region's exit).
+//   EMIT (pcap_emit_wide_kernel; pcap_emit_kernel with PKTGPU_PCAP_EMITR=0)  32 regions per block, up
+//            to 4 records per thread per pass with their list loads issued before the stores: offset =
+//            pos + 16, incl_len = next pos - pos - 16 (the last one from the region's exit).
 // tests/test_pcap_model.py restates the composition and the fixes and checks them against the host
 // indexer on captures built to defeat the guess.  HBM traffic ≈ the file once + 2 B/record of
 // record lists written and read + 12 B/record of output.
