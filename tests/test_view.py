@@ -92,3 +92,29 @@ def test_view_of_gpu_columns_vs_pyref():
         _check_against_pyref(sub, [bytes(buf[offs[i]:offs[i] + lens[i]]) for i in idx], "gpu c4")
     finally:
         P.close()
+
+
+@pytest.mark.gpu
+def test_view_of_gpu_columns_vs_oracle_columns():
+    """pkt_view over the HIP parse's chain columns equals pkt_view over the oracle's (the C
+    restatement of fast.rs pinned by the reference's own fixtures) for every packet of a C4 batch with
+    truncated records: the view the Rust adapter builds PacketSlice from is anchored on the oracle, not
+    only on the independent walk of tests/pyref.py."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.fail("no GPU visible")
+    P = pktgpu.Parser(0)
+    try:
+        n = 1 << 15
+        buf, offs, lens = gen.gen_c4(n, seed=12)
+        rng = np.random.default_rng(12)
+        cut = rng.random(n) < 0.05
+        lens = np.where(cut, (lens * rng.random(n)).astype(np.uint32), lens).astype(np.uint32)
+        g = P.parse(torch.from_numpy(buf).cuda(), offsets=torch.from_numpy(offs).cuda(),
+                    lens=torch.from_numpy(lens).cuda(), columns=["chain"])
+        host = {k: v.cpu().numpy() for k, v in g.items()}
+        ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, columns=list(host), nthreads=8)
+        for i in range(n):
+            assert pktgpu.view(host, i) == pktgpu.view(ref, i), i
+    finally:
+        P.close()
