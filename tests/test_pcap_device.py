@@ -303,3 +303,44 @@ def test_parse_pcap_span_staging_cap_past_count(P):
         else:
             assert np.array_equal(gv[:n], ov), k
             assert (gv[n:].view(np.uint8) == 0xEE).all(), k
+
+
+def test_epoch_wrap_past_2_16_calls():
+    """The scan blocks' published states carry a 16-bit call epoch (pktgpu_pcap.hip, BlkDesc) and the
+    scratch is cleared once when it wraps: 2^16 + 3 blocking calls on one ctx over a capture of several
+    scan blocks (with fake chains, so some regions are re-walked), the index checked against the host
+    indexer on the calls around the wrap and at the end — a state left by an older call must never
+    pass for the current one."""
+    import ctypes
+    import torch
+    import pktgpu
+    Q = pktgpu.Parser(0)  # a fresh ctx: its epoch starts at 0
+    try:
+        rng = np.random.default_rng(5)
+        pays = []
+        for i in range(9000):
+            pays.append(bytes(rng.integers(0, 256, int(rng.integers(40, 300)), dtype=np.uint8)))
+            if i % 97 == 0:  # a plausible-looking record header inside the payload (a fake chain)
+                pays[-1] = struct.pack("<IIII", 0, 5, 20, 20) + pays[-1][16:]
+        buf = records(pays)
+        o_ref, l_ref = gen.pcap_index_py(buf)
+        d = dev(buf)
+        n = len(o_ref)
+        o = torch.empty(n, dtype=torch.uint64, device="cuda")
+        l = torch.empty(n, dtype=torch.uint32, device="cuda")
+        cnt = ctypes.c_uint64()
+        s = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        L = Q._L
+        checks = {1, (1 << 16) - 2, (1 << 16) - 1, 1 << 16, (1 << 16) + 1, (1 << 16) + 3}
+        for call in range(1, (1 << 16) + 4):
+            if call in checks:
+                o.fill_(0)
+                l.fill_(0)
+            rc = L.pkt_pcap_index_device(Q._ctx, d.data_ptr(), d.numel(), o.data_ptr(), l.data_ptr(), n,
+                                         ctypes.byref(cnt), s)
+            assert rc == 0, call
+            if call in checks:
+                assert cnt.value == n, call
+                assert np.array_equal(o.cpu().numpy(), o_ref) and np.array_equal(l.cpu().numpy(), l_ref), call
+    finally:
+        Q.close()
