@@ -26,6 +26,7 @@ the capture in host memory ("host_pcap").
 Prints ONE JSON line (see DESIGN.md "Measurement" for every field).
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -427,14 +428,27 @@ def pcap_record(P, torch, dev, n=1 << 20, reps=10):
         ik.append(ms)
         ok = ok and ci == n
     ik = np.median(np.array(ik), axis=0)
+    # the same blocking call without the timing events (pkt_pcap_index_device): what a caller pays
+    cnt_u = ctypes.c_uint64()
+    su = ctypes.c_void_p(s.cuda_stream)
+    iu = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        rc = P._L.pkt_pcap_index_device(P._ctx, d_buf.data_ptr(), d_buf.numel(), d_offs.data_ptr(), d_lens.data_ptr(),
+                                        n, ctypes.byref(cnt_u), su)
+        iu.append(time.perf_counter() - t0)
+        ok = ok and rc == 0 and cnt_u.value == n
     index = {"entry": "pkt_pcap_index_device_timed (blocking, cap = n: offsets and lens written)",
              "ms_per_call": round(float(np.median(iw)) * 1e3, 4),
+             "ms_per_call_untimed": round(float(np.median(iu)) * 1e3, 4),
              "kernel_us": {"guess": round(float(ik[0]) * 1e3, 2), "scan": round(float(ik[1]) * 1e3, 2),
                            "emit": round(float(ik[2]) * 1e3, 2)},
              "kernels_us_total": round(float(ik.sum()) * 1e3, 2),
              "file_read_GB/s_guess": round(buf.size / (float(ik[0]) * 1e-3) / 1e9, 2),
              "timing": "wall clock per blocking call and HIP events recorded between the kernels on the "
-                       "call's stream, median of reps"}
+                       "call's stream (the events themselves add ~10 us to the call and to the kernels' "
+                       "spans: ms_per_call_untimed is pkt_pcap_index_device's, rocprof kernel averages in "
+                       "profiles/pcap/), median of reps"}
     # a stream of captures: pkt_parse_pcap_async on two ctxs / two streams, one capture in flight on
     # each, so one capture's index kernels overlap the other's parse (the C2 value's 2-stream form)
     import pktgpu
