@@ -227,6 +227,36 @@ def test_pcap_host_async_two_ctx(P):
         P2.close()
 
 
+def test_pcap_host_small_pieces_records_longer_than_a_piece(P):
+    """pkt_parse_pcap_host at the smallest piece (4096 B) over records of up to 9 KB: pieces that add
+    no record (their prefix's count does not move: an empty parse range and an empty export), records
+    and record headers split across several pieces, a file length that is no multiple of the piece;
+    every column, the index and the count equal the host indexer + the oracle."""
+    import struct
+    rng = np.random.default_rng(41)
+    tm = [pk.to_vec() for pk in gen.reference_22_packets()]
+    out_b = bytearray(gen.PCAP_GLOBAL_HEADER)
+    for i in range(1500):
+        body = tm[i % len(tm)] + bytes(int(rng.integers(0, 9000 if i % 5 == 0 else 300)))
+        out_b += struct.pack("<IIII", i, 0, len(body), len(body)) + body
+    buf = np.frombuffer(bytes(out_b), np.uint8)
+    offs, lens = gen.pcap_index_py(bytes(out_b))
+    n = len(offs)
+    hb = P.host_empty((buf.size,), np.uint8)
+    hb[:] = buf
+    out = {c: P.host_empty(schema.column_shape(c, n), schema.column_dtype(c)) for c in schema.COLUMN_NAMES}
+    P.set_host_piece(4096)
+    try:
+        assert buf.size % 4096 != 0 and int(lens.max()) > 2 * 4096
+        m, g, (o2, l2) = P.parse_pcap_host(hb, n, out=out)
+        assert m == n
+        assert np.array_equal(o2, offs) and np.array_equal(l2, lens)
+        ref = oracle.parse_batch(buf, n, offsets=offs, lens=lens, nthreads=8)
+        check(g, ref, "pcap host pieces of 4096 B, long records")
+    finally:
+        P.set_host_piece(0)
+
+
 @pytest.mark.parametrize("piece", [65537, 1 << 20])
 def test_pcap_host_pieces_vs_oracle(P, piece):
     """pkt_parse_pcap_host copies a capture in pieces and parses each prefix's new
