@@ -38,7 +38,8 @@ def run(a):
         t0 = time.perf_counter()
         P.parse_pcap(d_buf, n, out=out, offsets=d_offs, lens=d_lens, stream=s)
         ws.append(time.perf_counter() - t0)
-        time.sleep(0.002)  # separates the calls in the trace
+        if a.gap:
+            time.sleep(a.gap)  # separates the calls in the trace
     print(json.dumps({"what": "pkt_parse_pcap wall", "reps": a.reps, "median_us": round(float(np.median(ws)) * 1e6, 1),
                       "min_us": round(min(ws) * 1e6, 1)}), flush=True)
 
@@ -73,6 +74,7 @@ if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--records", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--gap", type=float, default=0.002, help="seconds between calls (0: back to back)")
     ap.add_argument("--trace", default=None, help="a rocprofv3 kernel_trace.csv of a run of this script")
     a = ap.parse_args()
     trace(a) if a.trace else run(a)
