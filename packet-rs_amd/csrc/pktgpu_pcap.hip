@@ -40,6 +40,7 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <type_traits>
 
 #include "pktgpu_ctx.hpp"
 
@@ -113,16 +114,29 @@ struct Scratch {
 //     `cnt` records, kBitBad if two of its regions disagree, kBitErr if a walk met a record
 //     running past the end of the file.  Consistent with e iff e == first and not bad.
 // combine(a, b) for a run a followed by run b is associative; none(0) is its identity.
-struct Agg {
-    uint64_t first, last, cnt;
+// F: the type of positions and counts in the scan's compositions — uint32_t for files shorter than
+// 4 GiB - 8 KiB (half the DPP moves and compare-selects per step: 74.4-75.1 vs 75.4-75.9 us per call,
+// profiles/ab/r05ar_pcap_scan_32bit.txt), uint64_t beyond (the host picks, pcap_launch).
+#ifndef PKTGPU_PCAP_AGG32
+#define PKTGPU_PCAP_AGG32 1
+#endif
+template <class F>
+struct AggT {
+    F first, last, cnt;
     uint32_t bits;
 };
-__device__ __forceinline__ Agg agg_identity() { return Agg{0, 0, 0, kBitNone}; }
+template <class F>
+__device__ __forceinline__ AggT<F> mk_agg(uint64_t f, uint64_t l, uint64_t c, uint32_t b) {
+    return AggT<F>{(F)f, (F)l, (F)c, b};
+}
+template <class F>
+__device__ __forceinline__ AggT<F> agg_identity() { return AggT<F>{0, 0, 0, kBitNone}; }
 // Without branches (selects; a "none" aggregate's first and cnt are 0): the scan steps, the
 // cross-wave loops and the look-back compose with no exec-mask save / restore per combine.
-__device__ __forceinline__ Agg combine(const Agg& a, const Agg& b) {
+template <class F>
+__device__ __forceinline__ AggT<F> combine(const AggT<F>& a, const AggT<F>& b) {
     const bool an = (a.bits & kBitNone) != 0, bn = (b.bits & kBitNone) != 0;
-    Agg r;
+    AggT<F> r;
     r.first = an ? b.first : a.first;
     r.last = an ? (bn ? (a.last > b.last ? a.last : b.last) : b.last) : (bn ? a.last : b.last);
     r.cnt = a.cnt + b.cnt;
@@ -425,11 +439,12 @@ __device__ __forceinline__ void st_agent(T* p, T v) {
 }
 
 // Region k's aggregate from its (entry, exit, count|err) state; identity past the file.
-__device__ __forceinline__ Agg region_agg(uint32_t k, uint32_t K, uint64_t entry, uint64_t exit, uint32_t cw) {
-    if (k >= K) return agg_identity();
+template <class F>
+__device__ __forceinline__ AggT<F> region_agg(uint32_t k, uint32_t K, uint64_t entry, uint64_t exit, uint32_t cw) {
+    if (k >= K) return agg_identity<F>();
     const uint64_t end = ((uint64_t)k + 1) * kRegion;
-    if (k != 0 && entry >= end) return Agg{0, end, 0, kBitNone};
-    return Agg{entry, exit, cw & kCntMask, (cw & kCntErr) ? kBitErr : 0u};
+    if (k != 0 && entry >= end) return mk_agg<F>(0, end, 0, kBitNone);
+    return mk_agg<F>(entry, exit, cw & kCntMask, (cw & kCntErr) ? kBitErr : 0u);
 }
 
 // The walk of one region by ONE lane (pcap_guess_kernel): pkt_pcap_index's loop from `entry` while the
@@ -758,12 +773,17 @@ __device__ __forceinline__ uint64_t dpp64(uint64_t old, uint64_t v) {
     return ((uint64_t)dpp32<CTRL, ROWS>((uint32_t)(old >> 32), (uint32_t)(v >> 32)) << 32) |
            dpp32<CTRL, ROWS>((uint32_t)old, (uint32_t)v);
 }
-template <int CTRL, int ROWS>
-__device__ __forceinline__ void scan_step(Agg& x, int32_t& ix) {
-    Agg y;
-    y.first = dpp64<CTRL, ROWS>(0, x.first);
-    y.last = dpp64<CTRL, ROWS>(0, x.last);
-    y.cnt = dpp64<CTRL, ROWS>(0, x.cnt);
+template <int CTRL, int ROWS, class F>
+__device__ __forceinline__ F dppf(F old, F v) {
+    if constexpr (sizeof(F) == 4) return dpp32<CTRL, ROWS>(old, v);
+    else return dpp64<CTRL, ROWS>(old, v);
+}
+template <int CTRL, int ROWS, class F>
+__device__ __forceinline__ void scan_step(AggT<F>& x, int32_t& ix) {
+    AggT<F> y;
+    y.first = dppf<CTRL, ROWS, F>(0, x.first);
+    y.last = dppf<CTRL, ROWS, F>(0, x.last);
+    y.cnt = dppf<CTRL, ROWS, F>(0, x.cnt);
     y.bits = dpp32<CTRL, ROWS>(kBitNone, x.bits);
     const int32_t iy = (int32_t)dpp32<CTRL, ROWS>(0xFFFFFFFFu, (uint32_t)ix);
     x = combine(y, x);
@@ -779,11 +799,12 @@ __device__ __forceinline__ uint64_t stamp_now() {
 }
 
 // (bx: diagnostic stamps — after the wave scans, after the first barrier — or NULL)
-__device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, int32_t* widx, Agg& total,
+template <class F>
+__device__ __forceinline__ AggT<F> block_exclusive(AggT<F> a, int32_t& idx, AggT<F>* wtot, int32_t* widx, AggT<F>& total,
                                                uint64_t* bx = nullptr) {
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     int32_t ix = (a.bits & kBitNone) ? -1 : (int32_t)t;
-    Agg x = a;
+    AggT<F> x = a;
     if constexpr (PKTGPU_PCAP_DPP) {
         scan_step<0x111, 0xF>(x, ix);  // row_shr:1
         scan_step<0x112, 0xF>(x, ix);  // row_shr:2
@@ -794,7 +815,7 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
     } else {
 #pragma unroll
     for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan within the wave
-        Agg y;
+        AggT<F> y;
         y.first = __shfl_up(x.first, d, 64);
         y.last = __shfl_up(x.last, d, 64);
         y.cnt = __shfl_up(x.cnt, d, 64);
@@ -815,9 +836,9 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
     if (PKTGPU_STAMPS && bx) bx[1] = stamp_now();
     // the waves' totals in order, one running composition (its value before wave w is this wave's
     // prefix): four combines, no loop branch
-    Agg before = agg_identity();
+    AggT<F> before = agg_identity<F>();
     int32_t ib = -1;
-    Agg run = agg_identity();
+    AggT<F> run = agg_identity<F>();
     int32_t irun = -1;
 #pragma unroll
     for (uint32_t q = 0; q < (uint32_t)kWaves; q++) {
@@ -831,12 +852,12 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
     }
     total = run;
     // exclusive: the wave prefix before this lane
-    Agg ex;
+    AggT<F> ex;
     int32_t iex;
     if constexpr (PKTGPU_PCAP_DPP) {  // wave_shr:1, lane 0 the identity
-        ex.first = dpp64<0x138, 0xF>(0, x.first);
-        ex.last = dpp64<0x138, 0xF>(0, x.last);
-        ex.cnt = dpp64<0x138, 0xF>(0, x.cnt);
+        ex.first = dppf<0x138, 0xF, F>(0, x.first);
+        ex.last = dppf<0x138, 0xF, F>(0, x.last);
+        ex.cnt = dppf<0x138, 0xF, F>(0, x.cnt);
         ex.bits = dpp32<0x138, 0xF>(kBitNone, x.bits);
         iex = (int32_t)dpp32<0x138, 0xF>(0xFFFFFFFFu, (uint32_t)ix);
     } else {
@@ -846,7 +867,7 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
         ex.bits = __shfl_up(x.bits, 1, 64);
         iex = __shfl_up(ix, 1, 64);
         if (lane == 0) {
-            ex = agg_identity();
+            ex = agg_identity<F>();
             iex = -1;
         }
     }
@@ -856,7 +877,8 @@ __device__ __forceinline__ Agg block_exclusive(Agg a, int32_t& idx, Agg* wtot, i
 }
 
 // Does a region with aggregate r disagree with the run `pre` before it (pre claiming)?
-__device__ __forceinline__ bool seam_bad(const Agg& pre, const Agg& r) {
+template <class F>
+__device__ __forceinline__ bool seam_bad(const AggT<F>& pre, const AggT<F>& r) {
     if (pre.bits & kBitNone) return false;
     return (r.bits & kBitNone) ? pre.last < r.last : pre.last != r.first;
 }
@@ -988,9 +1010,11 @@ __device__ __forceinline__ void coemit_block(uint32_t eb, uint32_t K, uint64_t c
 }
 
 // Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
+template <class F>
 __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                         uint32_t nb, int ticket, Scratch S, uint64_t cap,
                                                         uint64_t* __restrict__ offsets, uint32_t* __restrict__ lens) {
+    using Agg = AggT<F>;
     __shared__ uint4 lds[kWaves][kRegion / 16 + 2];
     __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
     __shared__ uint64_t sen[kScanRegions], sex[kScanRegions];
@@ -1095,7 +1119,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     // while that one agrees with its own left is re-walked from its exit; until no such region
     Agg total, pre_cur;  // pre_cur: the block-exclusive composition of the current states
     for (;;) {
-        const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
+        const Agg mine = region_agg<F>(k, K, sen[t], sex[t], scw[t]);
         int32_t j;
 #if PKTGPU_STAMPS
         const Agg pre = block_exclusive(mine, j, wtot, widx, total, t_bx ? nullptr : bx);
@@ -1137,9 +1161,9 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         st_agent(&my->a_cnt, tagged(S.epoch, total.cnt));
         st_agent(&my->a_bits, tagged(S.epoch, total.bits));
     }
-    Agg P = agg_identity();
+    Agg P = agg_identity<F>();
     for (;;) {
-        Agg acc = agg_identity();
+        Agg acc = agg_identity<F>();
         bool exact = blk == 0;
         uint64_t il = 0, ic = 0;
         uint32_t ib = 0;
@@ -1148,7 +1172,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             // window [hi - 256, hi): lane l of wave v reads block hi - 1 - 64 v - l
             const int64_t jj = hi - 1 - (int64_t)t;
             uint32_t st = 0;  // 0 unpublished, 1 aggregate, 2 exact
-            Agg a = agg_identity();
+            Agg a = agg_identity<F>();
             uint64_t xl = 0, xc = 0, xm = 0;
             // (PKTGPU_PCAP_SPIN: a lane whose block has published nothing yet re-reads it after a short
             // sleep, up to kSpinMax times, instead of the whole window being re-read after a block-wide retry)
@@ -1166,7 +1190,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                     xm = ib_ & kValMask;
                 } else if (tag_of(af) == ep && tag_of(al) == ep && tag_of(ac) == ep && tag_of(ab) == ep) {
                     st = 1;
-                    a = Agg{af & kValMask, al & kValMask, ac & kValMask, (uint32_t)(ab & 15u)};
+                    a = mk_agg<F>(af & kValMask, al & kValMask, ac & kValMask, (uint32_t)(ab & 15u));
                     // block 0's consistent aggregate IS its exact state (region 0 starts at 24 by
                     // definition; block 0 has no seam before it to fix): no wait for its exact
                     // state's publication, which a look-back's first read usually missed
@@ -1188,11 +1212,11 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             __syncthreads();
             const uint32_t near = s_near;
             if (jj >= 0 && t < near && st == 0) s_retry = 1;  // a nearer block has not published
-            if (t >= near) a = agg_identity();
+            if (t >= near) a = agg_identity<F>();
             // compose the window's aggregates after the nearest exact block in block order: thread
             // order is reversed block order — within a wave lane 63 is the earliest, and wave 3 the
             // earliest wave
-            Agg wr = agg_identity();
+            Agg wr = agg_identity<F>();
             {
                 Agg x = a;
 #pragma unroll
@@ -1202,7 +1226,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                     y.last = __shfl_down(x.last, dd, 64);
                     y.cnt = __shfl_down(x.cnt, dd, 64);
                     y.bits = __shfl_down(x.bits, dd, 64);
-                    if (lane + dd >= 64) y = agg_identity();
+                    if (lane + dd >= 64) y = agg_identity<F>();
                     x = combine(y, x);
                 }
                 if (lane == 0) wtot[w] = x;
@@ -1214,7 +1238,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             if (near < 256) {
                 exact = true;
                 if (t == near) {
-                    s_P = Agg{0, xl, xc, (uint32_t)xm & kBitErr};
+                    s_P = mk_agg<F>(0, xl, xc, (uint32_t)xm & kBitErr);
                 }
                 __syncthreads();
                 il = s_P.last;
@@ -1234,17 +1258,17 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             continue;
         }
         if (blk == 0) {
-            P = agg_identity();
+            P = agg_identity<F>();
             break;
         }
         // P = the exact state before this block: (exit, count, error)
         if (acc.bits & kBitNone) {
             if (il >= acc.last) {
-                P = Agg{0, il, ic, ib | 0u};
+                P = mk_agg<F>(0, il, ic, ib | 0u);
                 break;
             }
         } else if (!(acc.bits & kBitBad) && acc.first == il) {
-            P = Agg{0, acc.last, ic + acc.cnt, ib | (acc.bits & kBitErr)};
+            P = mk_agg<F>(0, acc.last, ic + acc.cnt, ib | (acc.bits & kBitErr));
             break;
         }
 #if PKTGPU_STAMPS
@@ -1255,11 +1279,11 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     PCAP_STAMP(3);
     // ---- this block's seams against the exact exit before it: fix the first disagreeing region
     // from the exact state before it, until none disagrees (exact by induction)
-    Agg exact_pre = blk == 0 ? agg_identity() : Agg{P.last, P.last, 0, 0};  // "claims" the exact exit
+    Agg exact_pre = blk == 0 ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0);  // "claims" the exact exit
     // (the states have not changed since the local fixes' last composition: reuse it, and recompose
     // only after a fix below)
     for (bool fresh = PKTGPU_PCAP_REUSE != 0;; fresh = false) {
-        const Agg mine = region_agg(k, K, sen[t], sex[t], scw[t]);
+        const Agg mine = region_agg<F>(k, K, sen[t], sex[t], scw[t]);
         if (!fresh) {
             int32_t j;
             pre_cur = block_exclusive(mine, j, wtot, widx, total);
@@ -1282,7 +1306,7 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         run_fixes();
     }
     // ---- the exact state after this block; each region's record prefix
-    const Agg all = combine(blk == 0 ? agg_identity() : Agg{P.last, P.last, 0, 0}, total);
+    const Agg all = combine(blk == 0 ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0), total);
     const uint64_t c_before = blk == 0 ? 0 : P.cnt;
     const uint32_t err_all = (P.bits | all.bits) & kBitErr;
     const uint64_t last = (all.bits & kBitNone) ? P.last : all.last;
@@ -1614,7 +1638,8 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     if (!pc.scan_resident) {  // scan blocks the device holds at once
         int per_cu = 0, cus = 0;
-        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_scan_kernel, 256, 0) != hipSuccess ||
+        // (the 64-bit build: at least the registers of the 32-bit one, so never more blocks)
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_scan_kernel<uint64_t>, 256, 0) != hipSuccess ||
             hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
             per_cu = cus = 0;
         pc.scan_resident = (uint32_t)std::max(1, per_cu * cus);
@@ -1626,8 +1651,13 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // e.g. the other ctx's capture of the async entries.  The occupancy test keeps the ticket for a
     // grid the device could not hold at once even alone.
     const uint32_t ne = (PKTGPU_PCAP_COEMIT && cap) ? (K + kCoEmitRegions - 1) / kCoEmitRegions : 0u;
-    hipLaunchKernelGGL(pcap_scan_kernel, dim3(nb + ne), blk, 0, s, buf, len, K, nb, nb > pc.scan_resident ? 1 : 0, S,
-                       cap, offsets, lens);
+    // 32-bit compositions while every position and count of the file fits (region ends included)
+    if (PKTGPU_PCAP_AGG32 && len + 2ull * kRegion < (1ull << 32))
+        hipLaunchKernelGGL(pcap_scan_kernel<uint32_t>, dim3(nb + ne), blk, 0, s, buf, len, K, nb,
+                           nb > pc.scan_resident ? 1 : 0, S, cap, offsets, lens);
+    else
+        hipLaunchKernelGGL(pcap_scan_kernel<uint64_t>, dim3(nb + ne), blk, 0, s, buf, len, K, nb,
+                           nb > pc.scan_resident ? 1 : 0, S, cap, offsets, lens);
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
