@@ -66,6 +66,10 @@ def parse_args():
     ap.add_argument("--streams", type=int, default=2,
                     help="consecutive steps are issued round-robin on this many HIP streams per device")
     ap.add_argument("--no-extra", action="store_true", help="skip the host and pcap records (N = 1)")
+    ap.add_argument("--virtual", action="store_true",
+                    help="TEST MODE: --gpus N shards on device 0 (pkt_mgpu_create_virtual, device copies instead "
+                         "of RCCL) to run the N-device code paths on one GPU; prints a line labelled as a smoke, "
+                         "never a measurement or a scaling point")
     return ap.parse_args()
 
 
@@ -593,14 +597,14 @@ def run_mgpu(args, ndev):
     """One process, ndev devices through pkt_mgpu (the measured form for every N)."""
     import torch
     visible = torch.cuda.device_count()
-    if visible < ndev:
+    if visible < ndev and not args.virtual:
         print(f"bench.py: --gpus {ndev} but only {visible} device(s) visible", file=sys.stderr)
         sys.exit(2)
     import pktgpu
     from pktgpu import mgpu, schema
     torch.cuda.set_device(0)
-    devices = list(range(ndev))
-    MP = mgpu.MultiParser(devices)
+    devices = [0] * ndev if args.virtual else list(range(ndev))
+    MP = mgpu.MultiParser(devices, virtual=args.virtual)
     MP.set_knobs(fastpath=args.fastpath, staging=args.staging, window=args.window)
     default_cols = DEFAULT_COLS[args.config]
     if args.columns is None:
@@ -730,6 +734,14 @@ def run_mgpu(args, ndev):
                              "device = the same K steps re-issued between one HIP event pair on device 0"}
     if c5 is not None:
         res["c5"] = c5
+    if args.virtual:
+        # a smoke of the N-shard code paths on one device: not the metric, not a scaling point
+        res["metric"] = f"VIRTUAL SMOKE (not a measurement): {ndev} shards on device 0 through pkt_mgpu_create_virtual"
+        res["n_gpus"] = 1
+        res["virtual_shards"] = ndev
+        res["scaling"] = None
+        res["config"]["parallelism"] = f"virtual{ndev} on one GPU"
+        res["config"]["launch"] += " (virtual handle: one physical device, gather messages by hipMemcpyAsync)"
     if ndev == 1 and not args.no_extra and args.config == "c2":
         # the other single-GPU BASELINE configs, device-resident, each with its own roofline
         for cfg in ("c3", "c4"):
@@ -909,7 +921,8 @@ def run_c5_mgpu(args, torch, MP, per, cols, entry):
                      "GB/s_into_root": round(sum(moved) / gather_s / 1e9, 2),
                      "rccl_messages": len(plan),
                      "backend": "RCCL (ncclCommInitAll, grouped ncclSend/ncclRecv over xGMI; at N = 1 the root's "
-                                "send to itself)",
+                                "send to itself)" if not MP.virtual else
+                                "VIRTUAL handle: hipMemcpyAsync on one device in place of RCCL (test mode)",
                      "root_copy": {"gather_ms": round(gather_c * 1e3, 4),
                                    "parse_plus_gather_ms": round(pg_c * 1e3, 4),
                                    "what": "pkt_mgpu_set_root_copy(1), the default: the root's own pieces by "
@@ -935,6 +948,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     ndev = world if world > 1 else args.gpus
+    if args.virtual and world > 1:
+        print("bench.py: --virtual runs in one process (no torch.distributed.run)", file=sys.stderr)
+        sys.exit(2)
     if world > 1 and world != args.gpus and rank == 0:
         print(f"bench.py: WORLD_SIZE={world} overrides --gpus {args.gpus}", file=sys.stderr)
     dist = None

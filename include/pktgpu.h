@@ -43,6 +43,7 @@ extern "C" {
 #define PKT_ERR_HIP           -2
 #define PKT_ERR_NO_DEVICE     -3
 #define PKT_ERR_UNSUPPORTED   -4
+#define PKT_ERR_GATHER_ROWS   -5  /* pkt_mgpu_synchronize: a packet had more headers than the fixed gather rows */
 
 /* Per-packet status (out->status). */
 typedef enum pkt_status {
@@ -571,6 +572,14 @@ int pkt_gather_plan(uint64_t col_mask, int nshards, const uint64_t *n, const uin
 typedef struct pkt_mgpu pkt_mgpu_t;
 /* `devices`: ndev distinct HIP device ids; index 0..ndev-1 into this list is the "shard" id. */
 int         pkt_mgpu_create(const int *devices, int ndev, pkt_mgpu_t **mg);
+/* TEST MODE (not a transport to measure): a handle whose device list may repeat a device (e.g. device 0
+ * listed 8 times: 8 shards, each with its own ctx and streams) and which holds no RCCL communicator:
+ * every gather message that pkt_mgpu_create's handle sends by ncclSend/ncclRecv is a hipMemcpyAsync on
+ * the sending shard's stream, ordered after the root's queued work and before the root's later work by
+ * events.  It runs the N-shard code paths (per-shard issuing threads, shard offsets, multi-shard gather
+ * plans and repack) on a one-GPU box; every other call behaves as for pkt_mgpu_create's handle. */
+int         pkt_mgpu_create_virtual(const int *devices, int ndev, pkt_mgpu_t **mg);
+int         pkt_mgpu_is_virtual(const pkt_mgpu_t *mg);
 int         pkt_mgpu_destroy(pkt_mgpu_t *mg);
 int         pkt_mgpu_ndev(const pkt_mgpu_t *mg);
 /* The handle's last error; pkt_mgpu_last_error(NULL) = why this thread's last pkt_mgpu_create failed. */
@@ -596,7 +605,10 @@ int pkt_mgpu_set_root_copy(pkt_mgpu_t *mg, int enable);
 /* Slot rows pkt_mgpu_parse_gather moves per shard: 0 (default) = each shard's largest n_hdrs, reduced
  * inside its parse kernel — the host waits once per device for it before issuing the gather; 1..16 =
  * that many rows for every shard (the caller's bound, >= every packet's n_hdrs; 16 always holds), so the
- * parse and the gather are queued with no host wait at all. */
+ * parse and the gather are queued with no host wait at all.  The largest n_hdrs is still reduced (when
+ * n_hdrs is among the columns) and the next pkt_mgpu_synchronize returns PKT_ERR_GATHER_ROWS if the last
+ * parse_gather had a packet with more headers than the fixed rows (its rows past them are unspecified in
+ * recv although its n_hdrs counts them). */
 int pkt_mgpu_set_gather_rows(pkt_mgpu_t *mg, int rows);
 /* Gather bytes[i] of send[i] (device memory of devices[i]) into `recv` on devices[root] at
  * recv_off[i] (recv_off NULL: consecutive blocks, each rounded up to 256 B), `recv_len` bytes.

@@ -31,6 +31,13 @@ struct pkt_mgpu {
     bool xinit = false;           // xs / xe all created (set only after every creation succeeded)
     int root_copy = 1;            // the root's own pieces: 1 = hipMemcpyAsync, 0 = RCCL send/recv to itself
     int gather_rows = 0;          // slot rows parse_gather moves: 0 = each shard's largest n_hdrs (waits), 1..16 fixed
+    // pkt_mgpu_set_gather_rows(k > 0): each shard's measured n_hdrs maximum of the last parse_gather (pinned
+    // words), checked against k by pkt_mgpu_synchronize once the streams have passed it
+    std::vector<const uint32_t*> rows_check;
+    // pkt_mgpu_create_virtual: no communicators; repeated devices allowed; the gather's messages are device
+    // copies on the sending shard's stream, ordered against the root's stream by one event per shard
+    bool virt = false;
+    std::vector<hipEvent_t> vev;
     // merge = 1: the root's staging area for the shards' packed buffers (the merge = 0 transfer) and
     // the repack table (pinned host copy, device copy; rp_ev = the last table upload has been read)
     int stage_dev = -1;
@@ -197,7 +204,8 @@ int pkt_shard_range(uint64_t n, int nshards, int i, uint64_t* lo, uint64_t* hi) 
     return PKT_SUCCESS;
 }
 
-int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
+namespace {
+int mgpu_create(const int* devices, int ndev, bool virt, pkt_mgpu_t** out) {
     g_create_err.clear();
     if (!out || !devices || ndev <= 0) return create_fail(PKT_ERR_INVALID_ARG, "null argument or ndev <= 0");
     *out = nullptr;
@@ -207,16 +215,19 @@ int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
         if (devices[i] < 0 || devices[i] >= count)
             return create_fail(PKT_ERR_INVALID_ARG, "device " + std::to_string(devices[i]) + " of " +
                                                         std::to_string(count) + " visible");
-        for (int j = 0; j < i; j++)
+        for (int j = 0; j < i && !virt; j++)
             if (devices[j] == devices[i])  // one communicator per device
                 return create_fail(PKT_ERR_INVALID_ARG, "device " + std::to_string(devices[i]) + " listed twice");
     }
     pkt_mgpu* mg = new pkt_mgpu();
     mg->ndev = ndev;
+    mg->virt = virt;
     mg->dev.assign(devices, devices + ndev);
     mg->ctx.assign(ndev, nullptr);
     mg->stream.assign(ndev, nullptr);
     mg->comm.assign(ndev, nullptr);
+    mg->vev.assign(virt ? ndev : 0, nullptr);
+    mg->rows_check.assign(ndev, nullptr);
     int rc = PKT_SUCCESS;
     std::string why;
     for (int i = 0; i < ndev && rc == PKT_SUCCESS; i++) {
@@ -227,12 +238,13 @@ int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
         }
         hipError_t e = hipSetDevice(devices[i]);
         if (e == hipSuccess) e = hipStreamCreateWithFlags(&mg->stream[i], hipStreamNonBlocking);
+        if (e == hipSuccess && virt) e = hipEventCreateWithFlags(&mg->vev[i], hipEventDisableTiming);
         if (e != hipSuccess) {
             rc = PKT_ERR_HIP;
-            why = std::string("hipStreamCreate: ") + hipGetErrorString(e);
+            why = std::string("hipStreamCreate / hipEventCreate: ") + hipGetErrorString(e);
         }
     }
-    if (rc == PKT_SUCCESS) {
+    if (rc == PKT_SUCCESS && !virt) {
         ncclResult_t r = ncclCommInitAll(mg->comm.data(), ndev, mg->dev.data());
         if (r != ncclSuccess) {
             for (auto& c : mg->comm) c = nullptr;
@@ -247,6 +259,15 @@ int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) {
     *out = mg;
     return PKT_SUCCESS;
 }
+}  // namespace
+
+int pkt_mgpu_create(const int* devices, int ndev, pkt_mgpu_t** out) { return mgpu_create(devices, ndev, false, out); }
+
+int pkt_mgpu_create_virtual(const int* devices, int ndev, pkt_mgpu_t** out) {
+    return mgpu_create(devices, ndev, true, out);
+}
+
+int pkt_mgpu_is_virtual(const pkt_mgpu_t* mg) { return mg && mg->virt ? 1 : 0; }
 
 int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
     if (!mg) return PKT_SUCCESS;
@@ -254,19 +275,24 @@ int pkt_mgpu_destroy(pkt_mgpu_t* mg) {
         (void)hipSetDevice(mg->dev[i]);
         if (mg->stream[i]) (void)hipStreamSynchronize(mg->stream[i]);
         for (size_t k = i * (pkt_mgpu::kMaxStreams - 1); k < mg->xs.size() && k < (i + 1) * (pkt_mgpu::kMaxStreams - 1ull); k++)
-            if (mg->xs[k]) {
-                (void)hipStreamSynchronize(mg->xs[k]);
-                (void)hipStreamDestroy(mg->xs[k]);
-            }
+            if (mg->xs[k]) (void)hipStreamSynchronize(mg->xs[k]);
+    }
+    // the root's staging area and repack table (once: a virtual handle lists the device several times)
+    if (mg->stage_dev != -1) {
+        (void)hipSetDevice(mg->stage_dev);
+        (void)hipDeviceSynchronize();
+        (void)hipFree(mg->stage);
+        (void)hipFree(mg->rp_dev);
+        (void)hipHostFree(mg->rp_host);
+        if (mg->rp_ev) (void)hipEventDestroy(mg->rp_ev);
+    }
+    for (int i = 0; i < mg->ndev; i++) {
+        (void)hipSetDevice(mg->dev[i]);
+        for (size_t k = i * (pkt_mgpu::kMaxStreams - 1); k < mg->xs.size() && k < (i + 1) * (pkt_mgpu::kMaxStreams - 1ull); k++)
+            if (mg->xs[k]) (void)hipStreamDestroy(mg->xs[k]);
         for (size_t k = i * pkt_mgpu::kMaxStreams; k < mg->xe.size() && k < (i + 1) * (size_t)pkt_mgpu::kMaxStreams; k++)
             if (mg->xe[k]) (void)hipEventDestroy(mg->xe[k]);
-        if (mg->dev[i] == mg->stage_dev) {
-            (void)hipDeviceSynchronize();
-            (void)hipFree(mg->stage);
-            (void)hipFree(mg->rp_dev);
-            (void)hipHostFree(mg->rp_host);
-            if (mg->rp_ev) (void)hipEventDestroy(mg->rp_ev);
-        }
+        if (i < (int)mg->vev.size() && mg->vev[i]) (void)hipEventDestroy(mg->vev[i]);
         if (mg->comm[i]) (void)ncclCommDestroy(mg->comm[i]);
         if (mg->stream[i]) (void)hipStreamDestroy(mg->stream[i]);
         if (mg->ctx[i]) pkt_ctx_destroy(mg->ctx[i]);
@@ -414,6 +440,39 @@ int pkt_mgpu_set_gather_rows(pkt_mgpu_t* mg, int rows) {
 }  // extern "C"
 
 namespace {
+// The virtual handle's transport (pkt_mgpu_create_virtual): the pieces issue_plan would send by RCCL, as
+// device copies on the sending shard's stream.  Like a grouped ncclSend/ncclRecv, shard i's copies start
+// after the work queued so far on both shard i's stream and the root's stream (the root's event), and the
+// root's stream waits for them (shard i's event) before anything queued on it later.
+int issue_copies(pkt_mgpu* mg, int root, const void* const* send, void* recv, const std::vector<pkt_gather_piece_t>& plan) {
+    const int nd = mg->ndev;
+    std::vector<char> has(nd, 0);
+    for (const pkt_gather_piece_t& p : plan)
+        if (p.shard != root || !mg->root_copy) has[p.shard] = 1;
+    hipError_t e = hipSetDevice(mg->dev[root]);
+    if (e == hipSuccess) e = hipEventRecord(mg->vev[root], mg->stream[root]);
+    if (e != hipSuccess) return mhip(mg, e, "hipEventRecord (virtual gather, root)");
+    for (int i = 0; i < nd; i++) {
+        if (!has[i]) continue;
+        const bool own = i == root;  // the root's own pieces (root copy off): on the root's stream, in order
+        if ((e = hipSetDevice(mg->dev[i])) != hipSuccess) return mhip(mg, e, "hipSetDevice (virtual gather)");
+        if (!own && (e = hipStreamWaitEvent(mg->stream[i], mg->vev[root], 0)) != hipSuccess)
+            return mhip(mg, e, "hipStreamWaitEvent (virtual gather)");
+        for (const pkt_gather_piece_t& p : plan) {
+            if (p.shard != i) continue;
+            e = hipMemcpyAsync(static_cast<uint8_t*>(recv) + p.dst, static_cast<const uint8_t*>(send[i]) + p.src, p.bytes,
+                               hipMemcpyDefault, mg->stream[i]);
+            if (e != hipSuccess) return mhip(mg, e, "hipMemcpyAsync (virtual gather)");
+        }
+        if (own) continue;
+        if ((e = hipEventRecord(mg->vev[i], mg->stream[i])) != hipSuccess) return mhip(mg, e, "hipEventRecord (virtual gather)");
+        if ((e = hipSetDevice(mg->dev[root])) != hipSuccess) return mhip(mg, e, "hipSetDevice (virtual gather)");
+        if ((e = hipStreamWaitEvent(mg->stream[root], mg->vev[i], 0)) != hipSuccess)
+            return mhip(mg, e, "hipStreamWaitEvent (virtual gather, root)");
+    }
+    return PKT_SUCCESS;
+}
+
 // Issue a gather plan: each piece from shard p.shard's buffer send[p.shard] + p.src to recv + p.dst
 // on the root.  The root's own pieces are device copies on the root stream (mg->root_copy) or RCCL
 // send/recv to itself; every other piece is a grouped ncclSend (the shard's stream) / ncclRecv (the
@@ -427,6 +486,7 @@ int issue_plan(pkt_mgpu* mg, int root, const void* const* send, void* recv, cons
                                    p.bytes, hipMemcpyDeviceToDevice, mg->stream[root]);
         if (e != hipSuccess) return mhip(mg, e, "hipMemcpyAsync (root shard)");
     }
+    if (mg->virt) return issue_copies(mg, root, send, recv, plan);
     ncclResult_t r = ncclGroupStart();
     if (r != ncclSuccess) return mnccl(mg, r, "ncclGroupStart");
     for (const pkt_gather_piece_t& p : plan) {
@@ -577,18 +637,23 @@ int pkt_mgpu_parse_gather(pkt_mgpu_t* mg, const pkt_batch_t* batches, int entry,
     // nothing, a PacketSlice holds exactly its headers): reduced inside the parse kernel and copied
     // to pinned host memory on the shard's stream; the host waits once per device, after every
     // shard's parse is queued.
-    // with a fixed row count (pkt_mgpu_set_gather_rows) nothing is measured and the host never waits
-    const bool nh = (mask >> 1 & 1) && mg->gather_rows == 0;
+    // with a fixed row count (pkt_mgpu_set_gather_rows) the host never waits: the count is still measured
+    // (same fused reduction) and pkt_mgpu_synchronize checks it against the fixed rows
+    const bool has_nh = mask >> 1 & 1;
+    const bool nh = has_nh && mg->gather_rows == 0;
+    const bool chk = has_nh && mg->gather_rows > 0;
     std::vector<uint32_t> rows(nd, mg->gather_rows ? (uint32_t)mg->gather_rows : PKT_MAX_HDRS);
     std::vector<const uint32_t*> rows_host(nd, nullptr);
+    std::fill(mg->rows_check.begin(), mg->rows_check.end(), nullptr);
     for (int i = 0; i < nd; i++) {
         if (!n[i]) continue;
         pkt_out_t o;
         pkt_out_packed(mask, n[i], shard_out[i], &o, nullptr);
-        const int rc = nh ? pktgpu_parse_rows_async(mg->ctx[i], &batches[i], entry, &o, mg->stream[i], &rows_host[i])
-                          : pkt_parse_batch(mg->ctx[i], &batches[i], entry, &o, mg->stream[i]);
+        const int rc = (nh || chk) ? pktgpu_parse_rows_async(mg->ctx[i], &batches[i], entry, &o, mg->stream[i], &rows_host[i])
+                                   : pkt_parse_batch(mg->ctx[i], &batches[i], entry, &o, mg->stream[i]);
         if (rc != PKT_SUCCESS)
             return mfail(mg, rc, "shard " + std::to_string(i) + ": " + pkt_ctx_last_error(mg->ctx[i]));
+        if (chk) mg->rows_check[i] = rows_host[i];
     }
     if (nh) {
         for (int i = 0; i < nd; i++) {
@@ -625,6 +690,21 @@ int pkt_mgpu_synchronize(pkt_mgpu_t* mg) {
         if (e == hipSuccess) e = hipStreamSynchronize(mg->stream[i]);
         if (e != hipSuccess) return mhip(mg, e, "hipStreamSynchronize");
     }
+    // the last parse_gather with fixed slot rows: did every packet fit them?
+    for (int i = 0; i < mg->ndev; i++) {
+        const uint32_t* w = mg->rows_check[i];
+        if (!w) continue;
+        uint32_t m = 0;
+        for (int k = 0; k < MaxScratch::kSpread; k++) m = std::max(m, w[k]);
+        if (m > (uint32_t)mg->gather_rows) {
+            std::fill(mg->rows_check.begin(), mg->rows_check.end(), nullptr);
+            return mfail(mg, PKT_ERR_GATHER_ROWS,
+                         "shard " + std::to_string(i) + ": a packet has " + std::to_string(m) +
+                             " headers, more than the gather's fixed " + std::to_string(mg->gather_rows) +
+                             " slot rows (pkt_mgpu_set_gather_rows): hdr_type / hdr_off rows past them were not gathered");
+        }
+    }
+    std::fill(mg->rows_check.begin(), mg->rows_check.end(), nullptr);
     return PKT_SUCCESS;
 }
 

@@ -139,6 +139,8 @@ SIGNATURES = {
     "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
     "pkt_mgpu_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
+    "pkt_mgpu_create_virtual": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
+    "pkt_mgpu_is_virtual": (ctypes.c_int, [_P]),
     "pkt_mgpu_destroy": (ctypes.c_int, [_P]),
     "pkt_mgpu_ndev": (ctypes.c_int, [_P]),
     "pkt_mgpu_last_error": (ctypes.c_char_p, [_P]),

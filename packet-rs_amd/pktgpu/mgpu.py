@@ -95,20 +95,28 @@ def shard_range(n, nshards, i):
 
 
 class MultiParser:
-    """A pkt_mgpu handle over a list of distinct HIP devices (one RCCL communicator each)."""
+    """A pkt_mgpu handle over a list of distinct HIP devices (one RCCL communicator each).
 
-    def __init__(self, devices):
+    virtual=True (TEST MODE, pkt_mgpu_create_virtual): the list may repeat a device — e.g. [0] * 8 is
+    eight shards on one GPU, each with its own ctx and streams — and the gather's messages are device
+    copies instead of RCCL, so the N-shard code paths run on a one-GPU box.  Not a measurement."""
+
+    def __init__(self, devices, virtual=False):
         torch = _torch()
         from . import _lib
         self._lib = _lib
         self._L = _lib.load()
         self.devices = [int(d) for d in devices]
+        self.virtual = bool(virtual)
         self.torch_devices = [torch.device("cuda", d) for d in self.devices]
         arr = (ctypes.c_int * len(self.devices))(*self.devices)
         h = ctypes.c_void_p()
-        rc = self._L.pkt_mgpu_create(arr, len(self.devices), ctypes.byref(h))
+        create = self._L.pkt_mgpu_create_virtual if self.virtual else self._L.pkt_mgpu_create
+        rc = create(arr, len(self.devices), ctypes.byref(h))
         if rc != 0:
-            raise RuntimeError(f"pkt_mgpu_create({self.devices}) failed: {rc}")
+            msg = self._L.pkt_mgpu_last_error(None)
+            raise RuntimeError(f"pkt_mgpu_create{'_virtual' if self.virtual else ''}({self.devices}) failed: {rc}: "
+                               f"{msg.decode() if msg else ''}")
         self._mg = h
 
     @property
@@ -166,42 +174,52 @@ class MultiParser:
 
     def _before_torch(self, tensors):
         """Order torch's current streams after the library's work, and tell the caching allocator
-        that every tensor the library touched is in use on the library's stream (so it is not
-        reused while a kernel or RCCL still reads or writes it)."""
+        that every tensor the library touched is in use on the library's streams of its device (so
+        it is not reused while a kernel, a copy or RCCL still reads or writes it)."""
         torch = _torch()
         ext = self.streams()
+        by_dev = {}
         for d, e in zip(self.torch_devices, ext):
             ev = torch.cuda.Event()
             ev.record(e)
             torch.cuda.current_stream(d).wait_event(ev)
-        by_dev = {d: e for d, e in zip(self.torch_devices, ext)}
+            by_dev.setdefault(d, []).append(e)
         for t in tensors:
             if t is not None and t.is_cuda and t.device in by_dev:
-                t.record_stream(by_dev[t.device])
+                for e in by_dev[t.device]:
+                    t.record_stream(e)
 
     # ---------------------------------------------------------------- inputs
-    def shard_fixed(self, slab, n, stride, lens=None):
+    def _bounds(self, n, bounds):
+        """[lo, hi) of every shard: the library's even split, or the caller's `bounds` (ndev + 1
+        non-decreasing record indices from 0 to n; uneven and empty shards allowed)."""
+        if bounds is None:
+            return [shard_range(n, self.ndev, i) for i in range(self.ndev)]
+        b = [int(x) for x in bounds]
+        if len(b) != self.ndev + 1 or b[0] != 0 or b[-1] != n or any(x > y for x, y in zip(b, b[1:])):
+            raise ValueError(f"bounds must be {self.ndev + 1} non-decreasing indices from 0 to {n}")
+        return list(zip(b[:-1], b[1:]))
+
+    def shard_fixed(self, slab, n, stride, lens=None, bounds=None):
         """Copy the contiguous shards of a host fixed-stride slab (numpy uint8) to the devices:
         [(slab tensor, n_i, stride, None, lens tensor|None)]."""
         torch = _torch()
         slab = np.ascontiguousarray(slab, np.uint8).reshape(-1)
         out = []
-        for i, dev in enumerate(self.torch_devices):
-            lo, hi = shard_range(n, self.ndev, i)
+        for i, (dev, (lo, hi)) in enumerate(zip(self.torch_devices, self._bounds(n, bounds))):
             s = torch.from_numpy(slab[lo * stride:hi * stride].copy()).to(dev) if hi > lo else \
                 torch.zeros(16, dtype=torch.uint8, device=dev)
             ln = torch.from_numpy(np.ascontiguousarray(lens[lo:hi], np.uint32)).to(dev) if lens is not None else None
             out.append((s, hi - lo, stride, None, ln))
         return out
 
-    def shard_indexed(self, buf, offsets, lens):
+    def shard_indexed(self, buf, offsets, lens, bounds=None):
         """Shards of an indexed (pcap) batch by record index; each device gets the whole file
         and its records' (offsets, lens)."""
         torch = _torch()
         a = np.ascontiguousarray(np.frombuffer(buf, np.uint8) if isinstance(buf, (bytes, bytearray)) else buf)
         out = []
-        for i, dev in enumerate(self.torch_devices):
-            lo, hi = shard_range(len(offsets), self.ndev, i)
+        for i, (dev, (lo, hi)) in enumerate(zip(self.torch_devices, self._bounds(len(offsets), bounds))):
             out.append((torch.from_numpy(a.copy()).to(dev), hi - lo, 0,
                         torch.from_numpy(np.ascontiguousarray(offsets[lo:hi], np.uint64)).to(dev),
                         torch.from_numpy(np.ascontiguousarray(lens[lo:hi], np.uint32)).to(dev)))
