@@ -275,6 +275,11 @@ int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
  * default (16 MiB), else any value >= 4096.  Results are identical for every value. */
 int         pkt_ctx_set_host_piece(pkt_ctx_t *ctx, uint64_t bytes);
 
+/* Tuning / test knob: 1 = the device pcap indexer composes its regions' states in 64-bit positions
+ * and counts for every file (the form files of 4 GiB and more always take), 0 (default) = 32-bit ones
+ * for files under 4 GiB.  Results are identical either way. */
+int         pkt_ctx_set_pcap_scan64(pkt_ctx_t *ctx, int enable);
+
 /* ---- the hot path ---- */
 /* fast::parse_<entry> over every packet of `batch`, writing the requested columns of `out`.
  * Asynchronous on `stream`; returns after the launch.  `batch` and `out` may also point into pinned
@@ -317,11 +322,13 @@ int pkt_parse_host(pkt_ctx_t *ctx, const pkt_batch_t *batch, int entry, const pk
  * the records' (data offset, incl_len).  *n_out = the record count (> cap: only the first cap are
  * parsed).  Blocking.  One host call at a time per ctx.
  * With pinned columns and a file longer than one piece (pkt_ctx_set_host_piece) the file is copied in
- * pieces and parsed while it arrives: once piece k has landed, the prefix [0, end of piece k) is
- * indexed (a record running past a prefix's end belongs to a later prefix) and the records it adds to
- * the previous prefix's are parsed, their columns flowing out over the link while piece k + 1 flows
- * in.  The last prefix is the whole file, indexed with pkt_pcap_index's errors; on such an error the
- * records of the earlier prefixes may already be written to `out`. */
+ * pieces and parsed while it arrives: once piece k has landed, the bytes it adds are indexed from the
+ * previous piece's carry on the device (the first record it could not count and its record count —
+ * pkt_pcap_stream_*'s steps; the file is indexed once, O(file), whatever the piece count; a record
+ * running past a piece's end belongs to a later piece) and the records it completes are parsed, their
+ * columns flowing out over the link while piece k + 1 flows in.  The last piece ends the file, indexed
+ * with pkt_pcap_index's errors; on such an error the records of the earlier pieces may already be
+ * written to `out`. */
 int pkt_parse_pcap_host(pkt_ctx_t *ctx, const uint8_t *buf, uint64_t len, int entry, const pkt_out_t *out,
                         uint64_t *offsets, uint32_t *lens, uint64_t cap, uint64_t *n_out);
 /* pkt_parse_pcap_host without the wait, for a stream of captures (cap <= 2^26, every column of `out`
@@ -560,6 +567,36 @@ typedef struct pkt_gather_piece {
 size_t pkt_sizeof_gather_piece(void);
 int pkt_gather_plan(uint64_t col_mask, int nshards, const uint64_t *n, const uint32_t *rows, int merge,
                     pkt_gather_piece_t *pieces, uint64_t cap, uint64_t *npieces, uint64_t *recv_bytes);
+
+/* ---- a capture that arrives in pieces (a NIC ring drained into host memory, a file read as it grows) ----
+ * The capture path of tests/pcap.rs:7-37 as a stream: bytes are pushed as they arrive and the device
+ * indexes and parses the records they complete while later bytes are still in flight.  Each step
+ * indexes only the new bytes: the device keeps the first record start a step could not count yet (a
+ * record running past the bytes so far) and the record count, and the next step starts the device
+ * indexer from them (no re-walk from offset 24: the whole capture is indexed once however many steps).
+ * The records, counts and errors are pkt_pcap_index's over the whole capture.
+ * open: a stream on `device` (its own ctx; pkt_pcap_stream_ctx gives it for the tuning knobs) for a
+ * capture of at most max_bytes (one device buffer) and `cap` records (<= 2^26; more are counted, not
+ * parsed); `out` = the requested columns for cap records (slot columns strided by cap), either all
+ * device memory of `device` (the parse writes them) or all pinned host memory from pkt_host_alloc (each
+ * step's columns are exported over the link while the next bytes copy in); step_bytes = new bytes that
+ * start a step at a push (0 = 4 MiB).
+ * push: append n bytes (host memory; the caller may reuse it when push returns).
+ * poll: a step over the bytes not yet indexed, then wait: *n_records = the records wholly inside the
+ * bytes so far (a record running past them is not an error yet), their columns written; offsets / lens
+ * (HOST, [cap], may be NULL) receive their (data offset, incl_len).
+ * finish: the capture is complete: a last step, the tail taken as pkt_pcap_index takes it (a record
+ * running past the end = PKT_ERR_INVALID_ARG; a partial record header is ignored), then as poll.
+ * Errors name the call in pkt_pcap_stream_last_error; after one, every later call returns it. */
+typedef struct pkt_pcap_stream pkt_pcap_stream_t;
+int         pkt_pcap_stream_open(int device, uint64_t max_bytes, uint64_t cap, int entry, const pkt_out_t *out,
+                                 uint64_t step_bytes, pkt_pcap_stream_t **st);
+int         pkt_pcap_stream_push(pkt_pcap_stream_t *st, const uint8_t *bytes, uint64_t n);
+int         pkt_pcap_stream_poll(pkt_pcap_stream_t *st, uint64_t *n_records, uint64_t *offsets, uint32_t *lens);
+int         pkt_pcap_stream_finish(pkt_pcap_stream_t *st, uint64_t *n_records, uint64_t *offsets, uint32_t *lens);
+pkt_ctx_t  *pkt_pcap_stream_ctx(pkt_pcap_stream_t *st);
+const char *pkt_pcap_stream_last_error(const pkt_pcap_stream_t *st);
+int         pkt_pcap_stream_close(pkt_pcap_stream_t *st);
 
 /* ---- multi-GPU: one process drives several devices ----
  * Every fast::parse_* is a pure function of one packet (fast.rs:5-227), so a batch splits into

@@ -290,125 +290,6 @@ __device__ __forceinline__ void stage_window(uint8_t* lds, uint32_t q, const u32
     }
 }
 
-// ---- block-staged column epilogue (build switch PKTGPU_LDS_COLS, the C2 column set) ----
-// The 25 per-packet columns of chain + Ether + IPv4 + UDP are first written into LDS as one run of 256
-// elements per column (the block's packets), then stored by 16-byte chunks: a u8 column's 256 B of a
-// block by 16 consecutive lanes, so a wave instruction writes 256-byte contiguous segments instead of
-// the 64 B (u8) / 128 B (u16) one per-lane narrow store writes (MI355X_MICROARCH: full store rate at
-// 256 contiguous bytes per wave instruction).  The runs are laid out by element size (u64, u32, u16,
-// u8: chunk j's column follows from j by three compares); slot rows stay per-lane stores.
-#ifndef PKTGPU_LDS_COLS
-#define PKTGPU_LDS_COLS 0
-#endif
-constexpr uint32_t kGmC2 = G_CHAIN | G_ETHER | G_IPV4 | G_UDP;
-enum StCol : uint32_t {
-    SC_ETH_DST, SC_ETH_SRC,                                                        // u64
-    SC_MASK, SC_V4SRC, SC_V4DST,                                                   // u32
-    SC_POFF, SC_PLEN, SC_ETYPE, SC_TLEN, SC_IDENT, SC_FRAG, SC_HCSUM, SC_CCALC,    // u16
-    SC_USRC, SC_UDST, SC_ULEN, SC_UCSUM,
-    SC_STATUS, SC_NHDRS, SC_VER, SC_IHL, SC_DIFF, SC_FLAGS, SC_TTL, SC_PROTO,      // u8
-    SC_N
-};
-__host__ __device__ constexpr uint32_t sc_size(uint32_t c) { return c < 2 ? 8u : c < 5 ? 4u : c < 17 ? 2u : 1u; }
-__host__ __device__ constexpr uint32_t sc_off(uint32_t c) {  // LDS byte offset of column c's run
-    return c < 2 ? 2048u * c : c < 5 ? 4096u + 1024u * (c - 2) : c < 17 ? 7168u + 512u * (c - 5) : 13312u + 256u * (c - 17);
-}
-constexpr uint32_t kStageBytes = 15360, kStageChunks = kStageBytes / 16;
-static_assert(sc_off(SC_N - 1) + 256u == kStageBytes && kStageBytes + 8u * SC_N <= 256u * 68u,
-              "the staging runs and the column table fit the C2 windows' LDS");
-__device__ __forceinline__ uint32_t chunk_col(uint32_t j) {
-    return j < 256u ? j >> 7 : j < 448u ? 2u + ((j - 256u) >> 6) : j < 832u ? 5u + ((j - 448u) >> 5) : 17u + ((j - 832u) >> 4);
-}
-__device__ __forceinline__ const void* sc_col(const pkt_out_t& o, uint32_t c) {
-    switch (c) {
-        case SC_ETH_DST: return o.eth_dst;
-        case SC_ETH_SRC: return o.eth_src;
-        case SC_MASK: return o.hdr_mask;
-        case SC_V4SRC: return o.ipv4_src;
-        case SC_V4DST: return o.ipv4_dst;
-        case SC_POFF: return o.payload_off;
-        case SC_PLEN: return o.payload_len;
-        case SC_ETYPE: return o.eth_etype;
-        case SC_TLEN: return o.ipv4_total_len;
-        case SC_IDENT: return o.ipv4_identification;
-        case SC_FRAG: return o.ipv4_frag_startset;
-        case SC_HCSUM: return o.ipv4_header_checksum;
-        case SC_CCALC: return o.ipv4_csum_calc;
-        case SC_USRC: return o.udp_src;
-        case SC_UDST: return o.udp_dst;
-        case SC_ULEN: return o.udp_length;
-        case SC_UCSUM: return o.udp_checksum;
-        case SC_STATUS: return o.status;
-        case SC_NHDRS: return o.n_hdrs;
-        case SC_VER: return o.ipv4_version;
-        case SC_IHL: return o.ipv4_ihl;
-        case SC_DIFF: return o.ipv4_diffserv;
-        case SC_FLAGS: return o.ipv4_flags;
-        case SC_TTL: return o.ipv4_ttl;
-        default: return o.ipv4_protocol;
-    }
-}
-// Thread t of a full 256-packet block: the emit of emit_chain + emit_fields<kGmC2> through the staging
-// runs (lds = the block's window region; every lane must have finished with its window: first barrier).
-template <class View>
-__device__ __forceinline__ void emit_staged_c2(const pkt_out_t& oc, uint32_t base, uint32_t t, uint32_t len,
-                                               const View& pv, const WalkResult& r, uint8_t* lds) {
-    const bool ok = r.status == PKT_OK;
-    uint32_t de[4] = {0, 0, 0, 0}, d4[5] = {0, 0, 0, 0, 0}, du[2] = {0, 0};
-    if (ok && r.f_eth >= 0) pv.template hdr<4>((uint32_t)r.f_eth, 14, de);
-    const bool h4 = ok && r.f_ipv4 >= 0;
-    if (h4) pv.template hdr<5>((uint32_t)r.f_ipv4, 20, d4);
-    if (ok && r.f_udp >= 0) pv.template hdr<2>((uint32_t)r.f_udp, 8, du);
-    __syncthreads();  // every lane has read its window: the region holds the staging runs from here
-    auto w8 = [&](uint32_t c, uint32_t v) { lds[sc_off(c) + t] = (uint8_t)v; };
-    auto w16 = [&](uint32_t c, uint32_t v) { *reinterpret_cast<uint16_t*>(lds + sc_off(c) + 2u * t) = (uint16_t)v; };
-    auto w32 = [&](uint32_t c, uint32_t v) { *reinterpret_cast<uint32_t*>(lds + sc_off(c) + 4u * t) = v; };
-    auto w64 = [&](uint32_t c, uint64_t v) { *reinterpret_cast<uint64_t*>(lds + sc_off(c) + 8u * t) = v; };
-    w8(SC_STATUS, r.status);
-    w8(SC_NHDRS, ok ? r.n : 0u);
-    w16(SC_POFF, ok ? r.payload_off : 0u);
-    w16(SC_PLEN, ok ? len - r.payload_off : 0u);
-    w32(SC_MASK, ok ? r.mask : 0u);
-    w64(SC_ETH_DST, ((uint64_t)de[0] << 16) | (de[1] >> 16));
-    w64(SC_ETH_SRC, ((uint64_t)(de[1] & 0xFFFFu) << 32) | de[2]);
-    w16(SC_ETYPE, de[3] >> 16);
-    w8(SC_VER, d4[0] >> 28);
-    w8(SC_IHL, (d4[0] >> 24) & 0xFu);
-    w8(SC_DIFF, (d4[0] >> 16) & 0xFFu);
-    w16(SC_TLEN, d4[0] & 0xFFFFu);
-    w16(SC_IDENT, d4[1] >> 16);
-    w8(SC_FLAGS, (d4[1] >> 13) & 7u);
-    w16(SC_FRAG, d4[1] & 0x1FFFu);
-    w8(SC_TTL, d4[2] >> 24);
-    w8(SC_PROTO, (d4[2] >> 16) & 0xFFu);
-    w16(SC_HCSUM, d4[2] & 0xFFFFu);
-    w32(SC_V4SRC, d4[3]);
-    w32(SC_V4DST, d4[4]);
-    {  // Packet::ipv4_checksum (packet.rs:93-107), the Q1 fold
-        uint32_t s = (d4[0] >> 16) + (d4[0] & 0xFFFFu) + (d4[1] >> 16) + (d4[1] & 0xFFFFu) + (d4[2] >> 16) +
-                     (d4[3] >> 16) + (d4[3] & 0xFFFFu) + (d4[4] >> 16) + (d4[4] & 0xFFFFu);
-        s = ((s >> 16) + s) & 0xFFFFu;
-        w16(SC_CCALC, h4 ? (~s & 0xFFFFu) : 0u);
-    }
-    w16(SC_USRC, du[0] >> 16);
-    w16(SC_UDST, du[0] & 0xFFFFu);
-    w16(SC_ULEN, du[1] >> 16);
-    w16(SC_UCSUM, du[1] & 0xFFFFu);
-    uint64_t* colp = reinterpret_cast<uint64_t*>(lds + kStageBytes);
-    if (t < SC_N) colp[t] = reinterpret_cast<uint64_t>(sc_col(oc, t)) + (uint64_t)base * sc_size(t);
-    __syncthreads();
-#pragma unroll
-    for (uint32_t k = 0; k < (kStageChunks + kBlock - 1) / kBlock; k++) {
-        const uint32_t j = k * kBlock + t;
-        if (j < kStageChunks) {
-            const uint32_t c = chunk_col(j);
-            const uint4 v = reinterpret_cast<const uint4*>(lds)[j];
-            uint4* g = reinterpret_cast<uint4*>(colp[c] + 16u * (j - (sc_off(c) >> 4)));
-            *as_global(g) = v;
-        }
-    }
-}
-
 // ---- several batches in one launch (pkt_parse_batches) ----
 // K batches of the same size and layout whose outputs lie at one common byte distance from batch
 // 0's (e.g. one packed output buffer each): block j parses tile j % bpb of batch j / bpb.  Every
@@ -643,24 +524,7 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
         const uint32_t m = wave_max_u32((active_own && r.status == PKT_OK) ? r.n : 0u);
         if ((t & 63u) == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
-    bool staged = false;
-    if constexpr (PKTGPU_LDS_COLS && GM == kGmC2 && LATE == L_SINGLE && NCH == 4) {
-        // a full block with aligned columns: every lane emits through the block's staging runs
-        if (p.stage_cols && base + (uint32_t)kBlock <= p.n) {
-            const uint64_t ka = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr()) + offsetof(KParams, out);
-            uint64_t kav = ka;
-            asm volatile("" : "+s"(kav));
-            const pkt_out_t KARG_AS* kc = reinterpret_cast<const pkt_out_t KARG_AS*>(kav);
-            pkt_out_t oc;
-            const void* const KARG_AS* kp = reinterpret_cast<const void* const KARG_AS*>(kc);
-            void** ocp = reinterpret_cast<void**>(&oc);
-#pragma unroll
-            for (int c = 0; c < 49; c++) ocp[c] = const_cast<void*>(kp[c]);
-            emit_staged_c2(oc, base, t, len_own, pv_own, r, lds);
-            staged = true;
-        }
-    }
-    if (active_own && !staged) {
+    if (active_own) {
         if constexpr (LATE != L_EARLY) {
             // The column bases are loaded here, after the walk, by scalar loads from the kernel
             // arguments (an opaque copy of their address keeps the loads from being hoisted to the
@@ -1050,11 +914,13 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         (void)hipFree(ctx->hp.file);
         (void)hipFree(ctx->hp.ioffs);
         (void)hipFree(ctx->hp.ilens);
-        (void)hipFree(ctx->hp.pcnt);
+        (void)hipFree(ctx->hp.pcarry);
         (void)hipFree(ctx->hp.pnh);
         (void)hipFree(ctx->hp.dcol);
-        for (uint32_t k = 0; k < 2 * ctx->hp.pev_n; k++) (void)hipEventDestroy(ctx->hp.pev[k]);
-        delete[] ctx->hp.pev;
+        if (ctx->hp.ev_copy) (void)hipEventDestroy(ctx->hp.ev_copy);
+        if (ctx->hp.ev_parsed) (void)hipEventDestroy(ctx->hp.ev_parsed);
+        for (hipEvent_t x : ctx->hp.ev_xdone)
+            if (x) (void)hipEventDestroy(x);
     }
     delete ctx;
     return PKT_SUCCESS;
@@ -1089,6 +955,12 @@ int pkt_ctx_set_walk(pkt_ctx_t* ctx, int mode) {
 int pkt_ctx_set_host_piece(pkt_ctx_t* ctx, uint64_t bytes) {
     if (!ctx || (bytes != 0 && bytes < 4096)) return PKT_ERR_INVALID_ARG;
     ctx->host_piece = bytes;
+    return PKT_SUCCESS;
+}
+
+int pkt_ctx_set_pcap_scan64(pkt_ctx_t* ctx, int enable) {
+    if (!ctx || enable < 0 || enable > 1) return PKT_ERR_INVALID_ARG;
+    ctx->pc.scan64 = enable != 0;
     return PKT_SUCCESS;
 }
 
@@ -1252,10 +1124,6 @@ static int parse_impl(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const pkt
         for (int c = 0; c < 49; c++)
             if (oc[c]) oc[c] += i0 * kColSize[c];
         kp.out = o;
-        // the block-staged epilogue (PKTGPU_LDS_COLS builds) stores whole 16-byte chunks of each column
-        kp.stage_cols = 1;
-        for (int c = 0; c < 49; c++)
-            if (c != kColHdrType && c != kColHdrOff && oc[c] && ((uintptr_t)oc[c] & 15)) kp.stage_cols = 0;
         if (mp) mp->base = kp;  // batch 0 of a multi-batch launch (n <= kLaunchChunk: one chunk)
         // the launch's grid: kp.n packets, or grid_n when the range starts at a device-produced index
         const uint32_t gn = (kp.n_dev && grid_n) ? (uint32_t)std::min<uint64_t>(grid_n, cnt) : kp.n;
@@ -1569,10 +1437,33 @@ static int pcap_host_buffers(pkt_ctx_t* ctx, uint64_t len, uint64_t cap) {
     return PKT_SUCCESS;
 }
 
+// A capture indexed and parsed as its bytes arrive (pkt_parse_pcap_host's pieces, pkt_pcap_stream_*), on
+// the ctx's three host streams: hp.s[1] copies bytes in; hp.s[0] runs one STEP per batch of new bytes —
+// the device indexer over the new regions only (segment mode: it starts from the previous step's carry,
+// the first record start that step did not count and its record count, kept in device words, so the
+// whole capture is indexed once, O(file), however many steps) and the parse of the records the step
+// added into the device columns; hp.s[2] exports those records' column ranges to the caller's pinned
+// columns in 16-byte chunks while the next bytes copy in (the link is full duplex).  The parse kernel
+// writing the host columns itself (its 1-8 B per-lane stores over the link) moved them at ~21 GB/s
+// against ~57 GB/s for wide chunks (profiles/host/r05b_pcap_host_pieces.jsonl).  The records a step adds
+// all end in (its start, its end] and are disjoint (>= 16 B each): at most (end - start) / 16 + 1 of
+// them, which sizes the step's parse grid.  Nothing on the host waits for the device between steps.
+struct Ingest {
+    pkt_ctx_t* ctx = nullptr;
+    int entry = 0;
+    uint64_t cap = 0;      // records the columns hold (slot rows strided by cap)
+    pkt_out_t dcols{};     // the parse's output: the caller's device columns or the ctx's hp.dcol
+    bool exporting = false;
+    ExportArgs xa{};       // exporting: hp.dcol -> the caller's pinned columns
+    uint64_t hi = 0;       // bytes copied to the device (hp.file[0, hi))
+    uint64_t indexed = 0;  // the prefix the last step indexed
+    uint64_t steps = 0;
+    int rc = PKT_SUCCESS;  // the first failure (every later call returns it)
+};
+constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
 static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
                             const pkt_out_t& hout, uint64_t* offsets, uint32_t* lens, uint64_t cap,
                             uint64_t* n_out, uint64_t piece, bool blocking);
-constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
 
 extern "C" {
 
@@ -1610,135 +1501,175 @@ int pkt_parse_pcap_host_result(pkt_ctx_t* ctx, uint64_t* n_out) {
 
 }  // extern "C"
 
-// pkt_parse_pcap_host with pinned columns, piece by piece (include/pktgpu.h), on the ctx's three host
-// streams: hp.s[1] copies piece k in; hp.s[0], once it has landed, indexes the prefix [0, hi_k)
-// (partial: a record running past hi_k is left to a later prefix; the last prefix is the file, with
-// the errors) into count word k and parses records [count k-1, count k) into DEVICE columns (the
-// caller's layout: slot rows strided by cap), reducing the piece's largest n_hdrs; hp.s[2] then exports
-// those records' column ranges to the caller's pinned columns in 16-byte chunks (export_kernel,
-// pktgpu_gather.hip) while the next pieces copy in — the link is full duplex.  The parse kernel writing
-// the host columns itself (its 1-8 B per-lane stores over the link) moved them at ~21 GB/s against
-// ~57 GB/s for wide chunks (profiles/host/r05b_pcap_host_pieces.jsonl).  The records a prefix adds all
-// end in (hi_{k-1}, hi_k] and are disjoint (>= 16 B each): at most (hi_k - hi_{k-1}) / 16 + 1 of them,
-// which sizes each parse's grid.
-// blocking = false (pkt_parse_pcap_host_async): everything queued, the capture left pending on the ctx.
+static int ingest_fail(Ingest& ig, int code) {  // nothing left in flight that reads the caller's bytes
+    HostPipe& hp = ig.ctx->hp;
+    for (int k = 0; k < HostPipe::kSlots; k++) (void)hipStreamSynchronize(hp.s[k]);
+    if (ig.rc == PKT_SUCCESS) ig.rc = code;
+    return code;
+}
+
+// The buffers, ring and events of a capture of up to len_cap bytes and cap records into `out`: pinned host
+// columns (hout = their device addresses: the parse writes hp.dcol, exported after each step) or the
+// caller's device columns (hout NULL: the parse writes them).  Waits for the ctx's earlier host-path work.
+static int ingest_begin(Ingest& ig, pkt_ctx_t* ctx, uint64_t len_cap, uint64_t cap, int entry, const pkt_out_t* out,
+                        const pkt_out_t* hout) {
+    ig.ctx = ctx;
+    ig.entry = entry;
+    ig.cap = cap;
+    ig.hi = ig.indexed = ig.steps = 0;
+    ig.rc = PKT_SUCCESS;
+    int rc = pcap_host_buffers(ctx, len_cap, cap);
+    if (rc != PKT_SUCCESS) return rc;
+    HostPipe& hp = ctx->hp;
+    hipError_t e = hipSuccess;
+    if (!hp.pcarry) e = hipMalloc(reinterpret_cast<void**>(&hp.pcarry), HostPipe::kRing * kPcapCarryWords * 8);
+    if (e == hipSuccess && !hp.pnh) e = hipMalloc(reinterpret_cast<void**>(&hp.pnh), HostPipe::kRing * kMaxSpread * 4);
+    if (e == hipSuccess && !hp.ev_copy) e = hipEventCreateWithFlags(&hp.ev_copy, hipEventDisableTiming);
+    if (e == hipSuccess && !hp.ev_parsed) e = hipEventCreateWithFlags(&hp.ev_parsed, hipEventDisableTiming);
+    for (int j = 0; j < HostPipe::kRing && e == hipSuccess; j++)
+        if (!hp.ev_xdone[j]) e = hipEventCreateWithFlags(&hp.ev_xdone[j], hipEventDisableTiming);
+    if (e != hipSuccess) return hip_fail(ctx, e, "capture ring");
+    ig.exporting = hout != nullptr;
+    if (!ig.exporting) {
+        ig.dcols = *out;
+    } else {
+        // the device columns: the requested ones, each at a 256-byte boundary, the caller's shapes
+        const uint8_t* const* hcol = reinterpret_cast<const uint8_t* const*>(out);
+        uint64_t coff[49], need = 0;
+        for (int c = 0; c < 49; c++) {
+            coff[c] = need;
+            if (hcol[c]) need += (col_bytes(c, cap) + 255) & ~(uint64_t)255;
+        }
+        if (need > hp.dcol_cap) {
+            (void)hipFree(hp.dcol);
+            hp.dcol = nullptr;
+            hp.dcol_cap = 0;
+            if ((e = hipMalloc(reinterpret_cast<void**>(&hp.dcol), need)) != hipSuccess)
+                return hip_fail(ctx, e, "hipMalloc (capture columns)");
+            hp.dcol_cap = need;
+        }
+        uint8_t** dc = reinterpret_cast<uint8_t**>(&ig.dcols);
+        const uint8_t* const* hc = reinterpret_cast<const uint8_t* const*>(hout);  // device-mapped host columns
+        ig.xa.ncol = 0;
+        ig.xa.cap = cap;
+        ig.xa.lo_h = ig.xa.hi_h = 0;
+        for (int c = 0; c < 49; c++) {
+            dc[c] = hcol[c] ? hp.dcol + coff[c] : nullptr;
+            if (!hcol[c]) continue;
+            const bool slot = c == kColHdrType || c == kColHdrOff;
+            for (uint32_t r = 0; r < (slot ? (uint32_t)PKT_MAX_HDRS : 1u); r++)
+                ig.xa.col[ig.xa.ncol++] = ExportCol{reinterpret_cast<uint64_t>(dc[c]) + (uint64_t)r * cap * kColSize[c],
+                                                    reinterpret_cast<uint64_t>(hc[c]) + (uint64_t)r * cap * kColSize[c],
+                                                    kColSize[c], slot ? r : kExportNoRow};
+        }
+    }
+    return pktgpu_pcap_reserve(ctx, len_cap, hp.s[0]);  // the whole capture's scratch: no growth between steps
+}
+
+// Copy the next n bytes of the capture in (hp.s[1], asynchronous: `src` must stay valid until the copy has
+// landed, hp.ev_copy).
+static int ingest_copy(Ingest& ig, const uint8_t* src, uint64_t n) {
+    if (ig.rc != PKT_SUCCESS) return ig.rc;
+    HostPipe& hp = ig.ctx->hp;
+    hipError_t e = hipMemcpyAsync(hp.file + ig.hi, src, n, hipMemcpyHostToDevice, hp.s[1]);
+    if (e == hipSuccess) e = hipEventRecord(hp.ev_copy, hp.s[1]);
+    if (e != hipSuccess) return ingest_fail(ig, hip_fail(ig.ctx, e, "hipMemcpyAsync H2D (capture bytes)"));
+    ig.hi += n;
+    return PKT_SUCCESS;
+}
+
+// One step over the bytes copied so far (last: the capture is complete — a record running past its end is
+// the capture's error; otherwise such a record waits for the next step).  Needs hi >= 24.
+static int ingest_step(Ingest& ig, bool last) {
+    if (ig.rc != PKT_SUCCESS) return ig.rc;
+    pkt_ctx_t* ctx = ig.ctx;
+    HostPipe& hp = ctx->hp;
+    hipStream_t cs = hp.s[1], ps = hp.s[0], es = hp.s[2];
+    (void)cs;
+    constexpr uint32_t R = HostPipe::kRing;
+    const uint64_t k = ig.steps;
+    const uint32_t j = (uint32_t)(k % R), jp = (uint32_t)((k + R - 1) % R);
+    const uint64_t region = pktgpu_pcap_region_bytes(), K = (ig.hi + region - 1) / region;
+    // the segment: from the region holding the previous step's end (its carry decides the exact entry),
+    // at least the last region (a final step with no new bytes still decides the carried record)
+    const uint32_t r0 = k ? (uint32_t)std::min<uint64_t>(ig.indexed / region, K - 1) : 0u;
+    hipError_t e = hipStreamWaitEvent(ps, hp.ev_copy, 0);
+    // the ring slot this step writes was last read by step k - R + 1's export
+    if (e == hipSuccess && ig.exporting && k + 1 >= R) e = hipStreamWaitEvent(ps, hp.ev_xdone[(k + 1) % R], 0);
+    if (e != hipSuccess) return ingest_fail(ig, hip_fail(ctx, e, "hipStreamWaitEvent (capture step)"));
+    uint64_t* carry = hp.pcarry + (uint64_t)j * kPcapCarryWords;
+    const uint64_t* cin = k ? hp.pcarry + (uint64_t)jp * kPcapCarryWords : nullptr;
+    const uint64_t* cnt = nullptr;
+    int rc = pktgpu_pcap_launch(ctx, hp.file, ig.hi, hp.ioffs, hp.ilens, ig.cap, ps, &cnt, !last, carry + 1, r0, cin, carry);
+    if (rc != PKT_SUCCESS) return ingest_fail(ig, rc);
+    pkt_batch_t db;
+    db.slab = hp.file;
+    db.slab_len = ig.hi;  // the prefix: every record parsed here lies inside it
+    db.offsets = hp.ioffs;
+    db.lens = hp.ilens;
+    db.stride = 0;
+    db.reserved = 0;
+    db.n = ig.cap;
+    uint32_t* nh = ig.exporting ? hp.pnh + (uint64_t)j * kMaxSpread : nullptr;
+    if (nh && (e = hipMemsetAsync(nh, 0, kMaxSpread * 4, ps)) != hipSuccess)
+        return ingest_fail(ig, hip_fail(ctx, e, "hipMemsetAsync"));
+    // the records this step added: [the previous step's count, this step's count)
+    rc = parse_impl(ctx, &db, ig.entry, &ig.dcols, ps, 0, ctx->staging, nh, ig.cap, nullptr, cnt, cin ? cin + 1 : nullptr,
+                    (ig.hi - ig.indexed) / 16 + 1);
+    if (rc != PKT_SUCCESS) return ingest_fail(ig, rc);
+    if (ig.exporting) {
+        if ((e = hipEventRecord(hp.ev_parsed, ps)) != hipSuccess || (e = hipStreamWaitEvent(es, hp.ev_parsed, 0)) != hipSuccess)
+            return ingest_fail(ig, hip_fail(ctx, e, "hipEventRecord (step parsed)"));
+        ig.xa.lo_dev = cin ? cin + 1 : nullptr;
+        ig.xa.hi_dev = cnt;
+        ig.xa.nhw = nh;
+        if ((e = pktgpu_export_launch(ig.xa, es)) != hipSuccess || (e = hipEventRecord(hp.ev_xdone[j], es)) != hipSuccess)
+            return ingest_fail(ig, hip_fail(ctx, e, "export_kernel"));
+    }
+    ig.indexed = ig.hi;
+    ig.steps++;
+    return PKT_SUCCESS;
+}
+
+// Wait for every queued step: the capture's outcome (pcap_finish: count, magic, a record past the end),
+// the index of the first min(count, cap) records copied to offsets / lens (host, may be NULL).
+static int ingest_wait(Ingest& ig, uint64_t* n_out, uint64_t* offsets, uint32_t* lens) {
+    if (ig.rc != PKT_SUCCESS) return ig.rc;
+    pkt_ctx_t* ctx = ig.ctx;
+    HostPipe& hp = ctx->hp;
+    hipError_t e = hipStreamSynchronize(hp.s[0]);
+    if (e != hipSuccess) return ingest_fail(ig, hip_fail(ctx, e, "hipStreamSynchronize"));
+    int rc = pktgpu_pcap_finish(ctx, n_out);
+    if (rc != PKT_SUCCESS) return ingest_fail(ig, rc);
+    const uint64_t m = std::min(*n_out, ig.cap);
+    if (m && offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
+        return ingest_fail(ig, hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)"));
+    if (m && lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, hp.s[1])) != hipSuccess)
+        return ingest_fail(ig, hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)"));
+    if ((e = hipStreamSynchronize(hp.s[1])) != hipSuccess || (e = hipStreamSynchronize(hp.s[2])) != hipSuccess)
+        return ingest_fail(ig, hip_fail(ctx, e, "hipStreamSynchronize"));
+    return PKT_SUCCESS;
+}
+
+// pkt_parse_pcap_host with pinned columns: the file copied in pieces of `piece` bytes, one step per piece
+// (blocking = false, pkt_parse_pcap_host_async: everything queued, the capture left pending on the ctx).
 static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int entry, const pkt_out_t* out,
                             const pkt_out_t& hout, uint64_t* offsets, uint32_t* lens, uint64_t cap,
                             uint64_t* n_out, uint64_t piece, bool blocking) {
-    HostPipe& hp = ctx->hp;
-    hipStream_t cs = hp.s[1], ps = hp.s[0], es = hp.s[2];
-    const uint64_t np64 = (len + piece - 1) / piece;
-    if (np64 > (1u << 20)) return fail(ctx, PKT_ERR_INVALID_ARG, "pkt_parse_pcap_host: too many pieces");
-    const uint32_t np = (uint32_t)np64;
-    hipError_t e = hipSuccess;
-    if (np > hp.pcnt_cap) {
-        (void)hipFree(hp.pcnt);
-        (void)hipFree(hp.pnh);
-        hp.pcnt = nullptr;
-        hp.pnh = nullptr;
-        hp.pcnt_cap = 0;
-        e = hipMalloc(reinterpret_cast<void**>(&hp.pcnt), (uint64_t)np * 8);
-        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void**>(&hp.pnh), (uint64_t)np * kMaxSpread * 4);
-        if (e != hipSuccess) return hip_fail(ctx, e, "hipMalloc (piece counts)");
-        hp.pcnt_cap = np;
-    }
-    if (np > hp.pev_n) {
-        hipEvent_t* ev = new hipEvent_t[2 * (size_t)np]();
-        for (uint32_t k = 0; k < 2 * hp.pev_n; k++) ev[k] = hp.pev[k];
-        delete[] hp.pev;
-        hp.pev = ev;
-        for (uint32_t k = hp.pev_n; k < np && e == hipSuccess; k++) {
-            e = hipEventCreateWithFlags(&hp.pev[2 * k], hipEventDisableTiming);
-            if (e == hipSuccess) e = hipEventCreateWithFlags(&hp.pev[2 * k + 1], hipEventDisableTiming);
-            if (e == hipSuccess) hp.pev_n = k + 1;
-        }
-        if (e != hipSuccess) return hip_fail(ctx, e, "hipEventCreate (pieces)");
-    }
-    // the device columns: the requested ones, each at a 256-byte boundary, the caller's shapes
-    const uint8_t* const* hcol = reinterpret_cast<const uint8_t* const*>(out);
-    uint64_t coff[49], need = 0;
-    for (int c = 0; c < 49; c++) {
-        coff[c] = need;
-        if (hcol[c]) need += (col_bytes(c, cap) + 255) & ~(uint64_t)255;
-    }
-    if (need > hp.dcol_cap) {
-        (void)hipFree(hp.dcol);
-        hp.dcol = nullptr;
-        hp.dcol_cap = 0;
-        if ((e = hipMalloc(reinterpret_cast<void**>(&hp.dcol), need)) != hipSuccess)
-            return hip_fail(ctx, e, "hipMalloc (capture columns)");
-        hp.dcol_cap = need;
-    }
-    pkt_out_t dcols;
-    uint8_t** dc = reinterpret_cast<uint8_t**>(&dcols);
-    const uint8_t* const* hc = reinterpret_cast<const uint8_t* const*>(&hout);  // device-mapped host columns
-    ExportArgs xa;
-    xa.ncol = 0;
-    xa.cap = cap;
-    xa.lo_h = xa.hi_h = 0;
-    for (int c = 0; c < 49; c++) {
-        dc[c] = hcol[c] ? hp.dcol + coff[c] : nullptr;
-        if (!hcol[c]) continue;
-        const bool slot = c == kColHdrType || c == kColHdrOff;
-        for (uint32_t r = 0; r < (slot ? (uint32_t)PKT_MAX_HDRS : 1u); r++)
-            xa.col[xa.ncol++] = ExportCol{reinterpret_cast<uint64_t>(dc[c]) + (uint64_t)r * cap * kColSize[c],
-                                          reinterpret_cast<uint64_t>(hc[c]) + (uint64_t)r * cap * kColSize[c],
-                                          kColSize[c], slot ? r : kExportNoRow};
-    }
-    int rc = pktgpu_pcap_reserve(ctx, len, ps);  // the whole file's scratch: no growth between prefixes
+    Ingest ig;
+    int rc = ingest_begin(ig, ctx, len, cap, entry, out, &hout);
     if (rc != PKT_SUCCESS) return rc;
-    auto bail = [&](int code) {  // nothing left in flight that reads `buf` or writes `out`
-        (void)hipStreamSynchronize(cs);
-        (void)hipStreamSynchronize(ps);
-        (void)hipStreamSynchronize(es);
-        return code;
-    };
-    uint64_t hi_prev = 0;
-    for (uint32_t k = 0; k < np; k++) {
-        const uint64_t lo = (uint64_t)k * piece, hi = std::min(len, lo + piece);
-        if ((e = hipMemcpyAsync(hp.file + lo, buf + lo, hi - lo, hipMemcpyHostToDevice, cs)) != hipSuccess ||
-            (e = hipEventRecord(hp.pev[2 * k], cs)) != hipSuccess || (e = hipStreamWaitEvent(ps, hp.pev[2 * k], 0)) != hipSuccess)
-            return bail(hip_fail(ctx, e, "hipMemcpyAsync H2D (pcap piece)"));
-        const bool last = k + 1 == np;
-        const uint64_t* cnt = nullptr;
-        if ((rc = pktgpu_pcap_launch(ctx, hp.file, hi, hp.ioffs, hp.ilens, cap, ps, &cnt, !last, hp.pcnt + k)) != PKT_SUCCESS)
-            return bail(rc);
-        pkt_batch_t db;
-        db.slab = hp.file;
-        db.slab_len = hi;  // the prefix: every record parsed here lies inside it
-        db.offsets = hp.ioffs;
-        db.lens = hp.ilens;
-        db.stride = 0;
-        db.reserved = 0;
-        db.n = cap;
-        uint32_t* nh = hp.pnh + (uint64_t)k * kMaxSpread;
-        if ((e = hipMemsetAsync(nh, 0, kMaxSpread * 4, ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipMemsetAsync"));
-        rc = parse_impl(ctx, &db, entry, &dcols, ps, 0, ctx->staging, nh, cap, nullptr, cnt,
-                        k ? hp.pcnt + (k - 1) : nullptr, (hi - hi_prev) / 16 + 1);
-        if (rc != PKT_SUCCESS) return bail(rc);
-        if ((e = hipEventRecord(hp.pev[2 * k + 1], ps)) != hipSuccess || (e = hipStreamWaitEvent(es, hp.pev[2 * k + 1], 0)) != hipSuccess)
-            return bail(hip_fail(ctx, e, "hipEventRecord (piece parsed)"));
-        xa.lo_dev = k ? hp.pcnt + (k - 1) : nullptr;
-        xa.hi_dev = cnt;
-        xa.nhw = nh;
-        if ((e = pktgpu_export_launch(xa, es)) != hipSuccess) return bail(hip_fail(ctx, e, "export_kernel"));
-        hi_prev = hi;
+    for (uint64_t lo = 0; lo < len; lo += piece) {
+        const uint64_t hi = std::min(len, lo + piece);
+        if ((rc = ingest_copy(ig, buf + lo, hi - lo)) != PKT_SUCCESS) return rc;
+        if ((rc = ingest_step(ig, hi == len)) != PKT_SUCCESS) return rc;
     }
     if (!blocking) {
         ctx->pc.pending = true;
-        ctx->pc.pending_stream = ps;
+        ctx->pc.pending_stream = ctx->hp.s[0];
         return PKT_SUCCESS;
     }
-    if ((e = hipStreamSynchronize(ps)) != hipSuccess) return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
-    if ((rc = pktgpu_pcap_finish(ctx, n_out)) != PKT_SUCCESS) return bail(rc);
-    const uint64_t m = std::min(*n_out, cap);
-    if (m && offsets && (e = hipMemcpyAsync(offsets, hp.ioffs, m * 8, hipMemcpyDeviceToHost, cs)) != hipSuccess)
-        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (offsets)"));
-    if (m && lens && (e = hipMemcpyAsync(lens, hp.ilens, m * 4, hipMemcpyDeviceToHost, cs)) != hipSuccess)
-        return bail(hip_fail(ctx, e, "hipMemcpyAsync D2H (lens)"));
-    if ((e = hipStreamSynchronize(cs)) != hipSuccess || (e = hipStreamSynchronize(es)) != hipSuccess)
-        return bail(hip_fail(ctx, e, "hipStreamSynchronize"));
-    return PKT_SUCCESS;
+    return ingest_wait(ig, n_out, offsets, lens);
 }
 
 extern "C" {
@@ -1800,6 +1731,101 @@ int pkt_parse_pcap_host(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, int en
     rc = staged_parse(ctx, &db, entry, out, 0, true, cap);
     if (rc != PKT_SUCCESS) return bail(rc);
     if ((e = hipStreamSynchronize(hp.s[1])) != hipSuccess) return hip_fail(ctx, e, "hipStreamSynchronize");
+    return PKT_SUCCESS;
+}
+
+}  // extern "C"
+
+// ---- a capture that arrives in pieces (pkt_pcap_stream_*, include/pktgpu.h) ----
+struct pkt_pcap_stream {
+    pkt_ctx_t* ctx = nullptr;  // its own: the open capture holds the ctx's index scratch and host pipeline
+    Ingest ig;
+    uint64_t max_bytes = 0;
+    uint64_t step = 0;  // bytes of new data that start a step at a push
+    bool done = false;
+    std::string err;
+};
+
+namespace {
+constexpr uint64_t kStreamStep = 4ull << 20;
+int st_fail(pkt_pcap_stream* st, int code, const std::string& msg) {
+    if (st) st->err = msg;
+    return code;
+}
+int st_ctx_fail(pkt_pcap_stream* st, int code) { return st_fail(st, code, st->ctx ? st->ctx->err : "ctx"); }
+}  // namespace
+
+extern "C" {
+
+int pkt_pcap_stream_open(int device, uint64_t max_bytes, uint64_t cap, int entry, const pkt_out_t* out,
+                         uint64_t step_bytes, pkt_pcap_stream_t** out_st) {
+    if (!out_st || !out || !cap || max_bytes < 24) return PKT_ERR_INVALID_ARG;
+    *out_st = nullptr;
+    if (entry < 0 || entry >= PKT_ENTRY_COUNT || cap > kLaunchChunk) return PKT_ERR_INVALID_ARG;
+    pkt_out_t dout;
+    const bool pinned = out_mapped(out, dout);
+    if (!pinned) {  // then every requested column is device memory (none mapped host memory)
+        const uint8_t* const* oc = reinterpret_cast<const uint8_t* const*>(out);
+        for (int c = 0; c < 49; c++) {
+            const uint8_t* unused = nullptr;
+            if (oc[c] && host_mapped(oc[c], unused)) return PKT_ERR_INVALID_ARG;  // mixed host / device columns
+        }
+    }
+    pkt_pcap_stream* st = new pkt_pcap_stream();
+    int rc = pkt_ctx_create(device, &st->ctx);
+    if (rc == PKT_SUCCESS) rc = ingest_begin(st->ig, st->ctx, max_bytes, cap, entry, out, pinned ? &dout : nullptr);
+    if (rc != PKT_SUCCESS) {
+        pkt_pcap_stream_close(st);
+        return rc;
+    }
+    st->max_bytes = max_bytes;
+    st->step = step_bytes ? step_bytes : kStreamStep;
+    *out_st = st;
+    return PKT_SUCCESS;
+}
+
+int pkt_pcap_stream_push(pkt_pcap_stream_t* st, const uint8_t* bytes, uint64_t n) {
+    if (!st || (n && !bytes)) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
+    if (st->done) return st_fail(st, PKT_ERR_INVALID_ARG, "the capture is finished");
+    if (n > st->max_bytes - st->ig.hi) return st_fail(st, PKT_ERR_INVALID_ARG, "push past the capture's max_bytes");
+    if (!n) return PKT_SUCCESS;
+    int rc = ingest_copy(st->ig, bytes, n);
+    // the caller may reuse its buffer once this returns
+    const hipError_t e = rc == PKT_SUCCESS ? hipEventSynchronize(st->ctx->hp.ev_copy) : hipSuccess;
+    if (e != hipSuccess) rc = ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventSynchronize (push)"));
+    if (rc == PKT_SUCCESS && st->ig.hi >= 24 && st->ig.hi - st->ig.indexed >= st->step) rc = ingest_step(st->ig, false);
+    return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);
+}
+
+int pkt_pcap_stream_poll(pkt_pcap_stream_t* st, uint64_t* n_records, uint64_t* offsets, uint32_t* lens) {
+    if (!st || !n_records) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
+    *n_records = 0;
+    if (st->ig.hi < 24) return st->ig.rc;  // not even the global header yet
+    int rc = PKT_SUCCESS;
+    if (!st->done && st->ig.hi > st->ig.indexed) rc = ingest_step(st->ig, false);
+    if (rc == PKT_SUCCESS) rc = ingest_wait(st->ig, n_records, offsets, lens);
+    return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);
+}
+
+int pkt_pcap_stream_finish(pkt_pcap_stream_t* st, uint64_t* n_records, uint64_t* offsets, uint32_t* lens) {
+    if (!st || !n_records) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
+    *n_records = 0;
+    if (st->ig.hi < 24) return st_fail(st, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
+    int rc = PKT_SUCCESS;
+    if (!st->done) rc = ingest_step(st->ig, true);  // the tail as pkt_pcap_index takes it (errors included)
+    st->done = true;
+    if (rc == PKT_SUCCESS) rc = ingest_wait(st->ig, n_records, offsets, lens);
+    return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);
+}
+
+pkt_ctx_t* pkt_pcap_stream_ctx(pkt_pcap_stream_t* st) { return st ? st->ctx : nullptr; }
+
+const char* pkt_pcap_stream_last_error(const pkt_pcap_stream_t* st) { return st ? st->err.c_str() : "null stream"; }
+
+int pkt_pcap_stream_close(pkt_pcap_stream_t* st) {
+    if (!st) return PKT_SUCCESS;
+    if (st->ctx) pkt_ctx_destroy(st->ctx);  // waits for its streams
+    delete st;
     return PKT_SUCCESS;
 }
 

@@ -24,13 +24,15 @@ struct HostPipe {
     uint64_t* ioffs = nullptr;
     uint32_t* ilens = nullptr;
     uint64_t file_cap = 0, idx_cap = 0;  // bytes; records
-    // the piecewise capture: one device count word per piece (the records of the file's prefix up to
-    // the piece's end), one copy-done event per piece
-    uint64_t* pcnt = nullptr;
-    uint32_t pcnt_cap = 0;
-    hipEvent_t* pev = nullptr;   // [2 * pev_n]: piece k landed (pev[2k]), piece k parsed (pev[2k + 1])
-    uint32_t pev_n = 0;
-    uint32_t* pnh = nullptr;     // [pcnt_cap][256]: each piece's n_hdrs maximum, spread
+    // a capture indexed and parsed as its bytes arrive (pkt_parse_pcap_host's pieces, pkt_pcap_stream_*,
+    // pktgpu.hip Ingest): a ring of kRing steps' carry words (the prefix's first uncounted record start,
+    // its record count, the magic check) and n_hdrs maxima, and the events ordering the steps' streams
+    static constexpr int kRing = 4;
+    uint64_t* pcarry = nullptr;  // [kRing][4]
+    uint32_t* pnh = nullptr;     // [kRing][256]: a step's n_hdrs maximum, spread
+    hipEvent_t ev_copy = nullptr;            // the bytes copied so far have landed
+    hipEvent_t ev_parsed = nullptr;          // the last step's records are parsed
+    hipEvent_t ev_xdone[kRing] = {};         // step j's export has read its ring slot
     uint8_t* dcol = nullptr;     // the capture's columns on the device (the export's source)
     uint64_t dcol_cap = 0;       // bytes
 };
@@ -45,7 +47,7 @@ struct PcapScratch {
     uint64_t* ctl_dev = nullptr;  // the same words as the device addresses them (the kernel writes them)
     uint32_t epoch = 0;           // per call: block states of older calls are ignored, not cleared
     uint32_t scan_resident = 0;   // scan-kernel blocks resident at once (0 = not yet queried)
-    uint32_t guess_resident = 0;  // persistent guess-kernel blocks resident at once (0 = not yet queried)
+    bool scan64 = false;          // pkt_ctx_set_pcap_scan64: 64-bit scan compositions for every file
     // a capture queued by pkt_parse_pcap_async / pkt_parse_pcap_host_async whose outcome (the words
     // above) has not been taken yet: no other index call may reuse the scratch until it is
     bool pending = false;
@@ -134,9 +136,16 @@ int pktgpu_parse_counted(pkt_ctx_t* ctx, const pkt_batch_t* b, int entry, const 
 // partial / count_out: index buf[0, len) as the PREFIX of a capture still arriving (a record running past
 // its end ends the index, no error) and write the record count to the device word count_out (NULL: the
 // ctx's own word, returned in *count_dev either way).  pktgpu_pcap_reserve: scratch for a file of len bytes.
+// r0 / carry_in / carry_out (segment mode): index only the regions [r0, ceil(len / region)) of the prefix,
+// from the previous prefix's carry words (carry_in: its first uncounted record start, its record count, the
+// magic check; r0 * region <= that prefix's end), writing this prefix's carry to carry_out (4 words, may be
+// NULL; count_out = carry_out + 1 keeps the count there too).  pktgpu_pcap_region_bytes: the region size.
 int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                        uint64_t cap, hipStream_t s, const uint64_t** count_dev, bool partial = false,
-                       uint64_t* count_out = nullptr);
+                       uint64_t* count_out = nullptr, uint32_t r0 = 0, const uint64_t* carry_in = nullptr,
+                       uint64_t* carry_out = nullptr);
+uint32_t pktgpu_pcap_region_bytes();
+constexpr int kPcapCarryWords = 4;  // [first uncounted record start, records, magic check, -]
 int pktgpu_pcap_reserve(pkt_ctx_t* ctx, uint64_t len, hipStream_t s);
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out);
 int pktgpu_pcap_take(pkt_ctx_t* ctx, uint64_t* n_out);  // a queued capture's outcome (waits; clears pending)

@@ -62,8 +62,6 @@ struct KParams {
     const uint64_t* i0_dev;  // non-NULL (with n_dev): this launch parses packets [*i0_dev, min(n, *n_dev)) —
                              // block b takes packets *i0_dev + 256 b ... (pkt_parse_pcap_host's pieces: the
                              // records a prefix index added to the one before)
-    uint32_t stage_cols;  // PKTGPU_LDS_COLS builds: the C2 column set's bases are 16-byte aligned (the
-                          // block-staged store epilogue may write them by 16-byte chunks)
     uint32_t* nh_max;  // non-NULL: the batch's largest n_hdrs (the used slot rows), spread over kMaxSpread
                        // words (wave maxima atomicMax'ed into word blockIdx % kMaxSpread; the host
                        // takes the max of the words)

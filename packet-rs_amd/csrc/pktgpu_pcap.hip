@@ -30,9 +30,13 @@
 //            publishes its exact state and writes each region's exact record prefix.  The last
 //            block writes the total and the error flag to pinned host words and the parse's count
 //            to a device word.
-//   EMIT (pcap_emit_wide_kernel; pcap_emit_kernel with PKTGPU_PCAP_EMITR=0)  32 regions per block, up
-//            to 4 records per thread per pass with their list loads issued before the stores: offset =
-//            pos + 16, incl_len = next pos - pos - 16 (the last one from the region's exit).
+//   EMIT (pcap_emit_wide_kernel)  32 regions per block, up to 4 records per thread per pass with their
+//            list loads issued before the stores: offset = pos + 16, incl_len = next pos - pos - 16 (the
+//            last one from the region's exit).
+// Variants measured and rejected in rounds 3-5 (a dual-candidate guess, a branch-free chain check, a
+// persistent prefetching guess kernel, walk priority, global record lists, record writes by the scan
+// blocks, an emit co-scheduled in the scan grid, the 16-region emit) are kept out of this file as
+// profiles/ab/r06_pcap_rejected_variants.patch, with their measurements under profiles/ab/.
 // tests/test_pcap_model.py restates the composition and the fixes and checks them against the host
 // indexer on captures built to defeat the guess.  HBM traffic ≈ the file once + 2 B/record of
 // record lists written and read + 12 B/record of output.
@@ -46,10 +50,7 @@
 
 namespace {
 
-#ifndef PKTGPU_PCAP_REGION
-#define PKTGPU_PCAP_REGION 4096
-#endif
-constexpr uint32_t kRegion = PKTGPU_PCAP_REGION;  // bytes of record starts per region
+constexpr uint32_t kRegion = 4096;  // bytes of record starts per region
 static_assert(kRegion % 16 == 0 && kRegion / 16 <= 65536, "u16 record lists");
 constexpr uint32_t kMaxRec = kRegion / 16;       // records per region (each >= 16 B apart)
 constexpr int kWaves = 4;                         // waves (regions) per 256-thread block
@@ -80,13 +81,9 @@ enum : uint32_t { kBitNone = 1, kBitErr = 2, kBitBad = 4 };
 constexpr uint32_t kCntErr = 0x80000000u, kCntMask = 0x7FFFFFFFu;
 
 constexpr uint32_t kScanRegions = 256;  // regions per scan block (one per thread)
-constexpr uint32_t kEmitRegions = 16;   // regions per emit block
-#ifndef PKTGPU_PCAP_EMITR
-#define PKTGPU_PCAP_EMITR 32  // 0: pcap_emit_kernel; 75.3-75.8 vs 76.5-76.6 us per call (profiles/ab/r05s_pcap_emit_wide.txt)
-#endif
-#ifndef PKTGPU_PCAP_EMITPER
-#define PKTGPU_PCAP_EMITPER 4
-#endif
+// emit: regions per block and records per thread per pass (32 x 4: 75.3-75.8 us per call against
+// 76.5-76.6 for 16 regions one record per step, profiles/ab/r05s_pcap_emit_wide.txt)
+constexpr uint32_t kEmitRegions = 32, kEmitPer = 4;
 
 struct Scratch {
     uint64_t* rentry;  // per region: the walk's entry (>= the region's end: no record starts in it)
@@ -101,11 +98,23 @@ struct Scratch {
                        // an error), [1] the magic check (guess region 0)
     uint64_t* count_out;  // where the last scan block writes that count (dev + 0 unless the caller names a word)
     uint32_t epoch;
-    // partial = 1: the buffer is a PREFIX of a capture still arriving (pkt_parse_pcap_host's pieces): a
-    // record running past its end ends the index without an error (the walks' error bit is dropped, so
-    // the record is neither counted nor an error) — the records counted are those wholly inside it
+    // partial = 1: the buffer is a PREFIX of a capture still arriving (pkt_parse_pcap_host's pieces,
+    // pkt_pcap_stream_*): a record running past its end ends the index without an error — the records
+    // counted are those wholly inside it.  (The walks keep their error bit and the overrunning record's
+    // start in the slot after the region's records; only the verdict ignores it.)
     uint32_t partial;
+    // Segment mode (carry_in != NULL): the regions [r0, K) of the prefix buf[0, len) are indexed on from
+    // the previous prefix's carry — the first record start it did not count (B) and the records it
+    // counted (C), on the device — instead of the whole prefix from offset 24.  Every record starting
+    // before region r0 other than B's was counted (r0 * kRegion <= the previous prefix's end), and the
+    // record after B starts past that end, so B and its record decide region r0's exact entry and the
+    // exact state before the segment.  carry_out (may be NULL): this prefix's carry for the next segment.
+    uint32_t r0;
+    const uint64_t* carry_in;  // [kCarryB], [kCarryC], [kCarryMagic]
+    uint64_t* carry_out;
 };
+// A prefix's carry words (pcap_launch's carry_in / carry_out)
+enum : int { kCarryB = 0, kCarryC = 1, kCarryMagic = 2, kCarryWords = 4 };
 
 // The aggregate of a run of regions:
 //   none (kBitNone): no region of the run claims a record start; consistent with a predecessor
@@ -116,10 +125,8 @@ struct Scratch {
 // combine(a, b) for a run a followed by run b is associative; none(0) is its identity.
 // F: the type of positions and counts in the scan's compositions — uint32_t for files shorter than
 // 4 GiB - 8 KiB (half the DPP moves and compare-selects per step: 74.4-75.1 vs 75.4-75.9 us per call,
-// profiles/ab/r05ar_pcap_scan_32bit.txt), uint64_t beyond (the host picks, pcap_launch).
-#ifndef PKTGPU_PCAP_AGG32
-#define PKTGPU_PCAP_AGG32 1
-#endif
+// profiles/ab/r05ar_pcap_scan_32bit.txt), uint64_t beyond or when pkt_ctx_set_pcap_scan64 asks for it
+// (the host picks, pcap_launch).
 template <class F>
 struct AggT {
     F first, last, cnt;
@@ -221,33 +228,6 @@ __device__ __forceinline__ int chain_local(const uint32_t* lw, uint32_t c, uint3
     return 1;
 }
 
-// chain_local for kMinHops == kMaxHops == 2 without branches: both headers are read by every lane
-// (the second from a safe in-LDS address when the first is implausible or the chain leaves the staged
-// bytes) and the verdict is one select chain — the looped form's early returns made every
-// 64-candidate step pay exec-mask saves and restores for each hop.
-#ifndef PKTGPU_PCAP_RUNLAST
-#define PKTGPU_PCAP_RUNLAST 1  // pcapn main vs run-last: 83.5-84.2 vs 81.9-82.7 us per call (profiles/ab/r05g_pcap_guess_runlast.txt)
-#endif
-#ifndef PKTGPU_PCAP_RUNACROSS
-#define PKTGPU_PCAP_RUNACROSS 1  // the run goes on past the step's lane 63 (0: round-5 r05g form, for A/B)
-#endif
-#ifndef PKTGPU_PCAP_DUAL
-#define PKTGPU_PCAP_DUAL 0  // measured slower: 87.9 vs 82.2 us per call (profiles/ab/r05m_pcap_lookback_spin.txt)
-#endif
-#ifndef PKTGPU_PCAP_BRANCHFREE
-#define PKTGPU_PCAP_BRANCHFREE 0  // measured: 91.3 vs 89.9 us per call with it (r04a), kept for A/B
-#endif
-__device__ __forceinline__ int chain_local2(const uint32_t* lw, uint32_t c, uint32_t lend, uint32_t lim, uint32_t snap) {
-    if (c + 16 > lim) return 1;  // the file ends first (the caller guarantees c < lend)
-    const RecHdr h0 = hdr_lds(lw, c);
-    const bool ok0 = plausible32(h0, c, lim, snap);
-    const uint32_t p1 = c + 16 + h0.incl;  // < 2^22 past c when ok0 (incl <= 1 MiB)
-    const bool end1 = p1 + 16 > lim, far1 = p1 >= lend;
-    const RecHdr h1 = hdr_lds(lw, (ok0 & !end1 & !far1) ? p1 : c);
-    const bool ok1 = plausible32(h1, p1, lim, snap) & (h1.sec - h0.sec + kTsSpan <= 2 * kTsSpan);
-    return !ok0 ? 0 : end1 ? 1 : far1 ? 2 : (ok1 ? 1 : 0);
-}
-
 __device__ __forceinline__ bool chain_global(const uint32_t* lw, const uint8_t* buf, uint64_t lbase, uint64_t lend,
                                              uint64_t c, uint64_t stop, uint64_t len, uint32_t snap) {
     uint64_t p = c;
@@ -306,13 +286,13 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
         while (q < lim) {
             const uint32_t k2 = (q >> 2) + 2;
             const uint32_t incl = __builtin_amdgcn_alignbyte(lr[k2 + 1], lr[k2], q);
+            rv = lane == c ? q : rv;  // (an overrunning record's start too: slot c, not counted)
+            if (c >= 64u && c < kMaxRec && lane == 0) list[c] = (uint16_t)q;
             if (incl > room - 16 - q) {  // pkt_pcap_index: record runs past the end
                 e = 1;
                 q = room;
                 break;
             }
-            rv = lane == c ? q : rv;
-            if (c >= 64u && c < kMaxRec && lane == 0) list[c] = (uint16_t)q;
             c++;
             q += 16 + incl;
         }
@@ -330,14 +310,14 @@ __device__ __forceinline__ void walk(const uint32_t* lw, uint64_t lbase, uint16_
     const uint32_t lane = lane_id();
     while (pos < end && pos + 16 <= len) {
         const uint32_t incl = ld32(lw, (uint32_t)(pos - lbase) + 8);
+        const uint32_t ro = (uint32_t)(pos - base);
+        rec = lane == cnt ? ro : rec;  // (an overrunning record's start too: slot cnt, not counted)
+        if (__builtin_amdgcn_readfirstlane(cnt) >= 64u && cnt < kMaxRec && lane == 0) list[cnt] = (uint16_t)ro;
         if (pos + 16 + (uint64_t)incl > len) {  // pkt_pcap_index: record runs past the end
             err = 1;
             pos = len;
             break;
         }
-        const uint32_t ro = (uint32_t)(pos - base);
-        rec = lane == cnt ? ro : rec;
-        if (__builtin_amdgcn_readfirstlane(cnt) >= 64u && cnt < kMaxRec && lane == 0) list[cnt] = (uint16_t)ro;
         cnt++;
         pos += 16 + (uint64_t)incl;
     }
@@ -366,7 +346,6 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
         // there is none do the candidates whose chains leave them read global memory.
         uint64_t m = __ballot(r == 1);
         if (!m) m = __ballot(r == 2 && chain_global(lw, buf, lbase, lend, c, stop, len, snap));
-#if PKTGPU_PCAP_RUNLAST
         // The lowest verified candidate, moved to the LAST of the run of consecutive verified
         // candidates it starts: a record whose predecessor's payload ends in zero bytes verifies one
         // to three bytes early too (its fields shifted by whole bytes stay plausible), and the
@@ -381,44 +360,21 @@ __device__ __forceinline__ uint64_t guess_entry(const uint8_t* __restrict__ buf,
             const uint32_t f = run != kNoRun ? 0u : (uint32_t)__builtin_ctzll(m);
             const uint64_t rest = ~(m >> f);  // bit j clear iff candidate f + j verified (j < 64 - f)
             const uint32_t rl = rest ? (uint32_t)__builtin_ctzll(rest) : 64u;  // the run's length
-            if (f + rl < 64u || !PKTGPU_PCAP_RUNACROSS) {
+            if (f + rl < 64u) {
                 res = c0 + f + rl - 1u;
                 return true;
             }
             run = c0 + 63;
         }
-#else
-        if (m) {
-            res = c0 + (uint64_t)__builtin_ctzll(m);
-            return true;
-        }
-#endif
         return false;
     };
     uint64_t res = 0;
-    if constexpr (PKTGPU_PCAP_DUAL && kMinHops == 2 && kMaxHops == 2) {
-        // two steps' candidates per lane checked together (two independent branch-free chains: their
-        // LDS reads overlap), then decided in step order
-        for (uint64_t c0 = base; c0 < stop; c0 += 128) {
-            const uint64_t ca = c0 + lane, cb = ca + 64;
-            const int ra = ca < stop && ca + 16 <= len ? chain_local2(lw, (uint32_t)(ca - lbase), STAGED, lim, snap) : 0;
-            const int rb = cb < stop && cb + 16 <= len ? chain_local2(lw, (uint32_t)(cb - lbase), STAGED, lim, snap) : 0;
-            if (step(ra, ca, c0, res)) return res;
-            if (c0 + 64 >= stop) break;
-            if (step(rb, cb, c0 + 64, res)) return res;
-        }
-    } else {
-        for (uint64_t c0 = base; c0 < stop; c0 += 64) {
-            const uint64_t c = c0 + lane;
-            int r = 0;
-            if constexpr (PKTGPU_PCAP_BRANCHFREE && kMinHops == 2 && kMaxHops == 2)
-                r = c < stop && c + 16 <= len ? chain_local2(lw, (uint32_t)(c - lbase), STAGED, lim, snap) : 0;
-            else
-                r = c < stop && c + 16 <= len
-                        ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
-                        : 0;
-            if (step(r, c, c0, res)) return res;
-        }
+    for (uint64_t c0 = base; c0 < stop; c0 += 64) {
+        const uint64_t c = c0 + lane;
+        const int r = c < stop && c + 16 <= len
+                          ? chain_local(lw, (uint32_t)(c - lbase), (uint32_t)(stop - lbase), STAGED, lim, snap)
+                          : 0;
+        if (step(r, c, c0, res)) return res;
     }
     return run != kNoRun ? run : base + kRegion;
 }
@@ -460,12 +416,12 @@ __device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, ui
     while (q < lim) {
         const uint32_t k2 = (q >> 2) + 2;
         const uint32_t incl = __builtin_amdgcn_alignbyte(lr[k2 + 1], lr[k2], q);
+        lst[c] = (uint16_t)q;  // (an overrunning record's start too: slot c, not counted)
         if (incl > room - 16 - q) {  // pkt_pcap_index: record runs past the end
             e = 1;
             q = room;
             break;
         }
-        lst[c] = (uint16_t)q;
         c++;
         q += 16 + incl;
     }
@@ -473,20 +429,12 @@ __device__ __forceinline__ void lane_walk(const uint32_t* lw, uint64_t lbase, ui
     cnt = c | (e ? kCntErr : 0u);
 }
 
-// lane_walk without branches (PKTGPU_PCAP_WALK2): the walking lanes run a loop whose trip count is
+// lane_walk without branches (files below 2 GiB): the walking lanes run a loop whose trip count is
 // uniform (until no lane is active, two hops per test); a finished lane reads a safe LDS address and
 // stores its would-be offset to a dummy slot (lst[kMaxRec]), so a hop is one ds_read2, the
 // arithmetic and one ds_write with no exec-mask save/restore (the branchy loop above spent ~25
 // scalar and vector instructions per hop on them, ~380 cycles per hop in the guess kernel's
 // stamps: profiles/pcap/r04m_stamps.txt).  `valid` = the lane has a region to walk.
-#ifndef PKTGPU_PCAP_WALK2
-#define PKTGPU_PCAP_WALK2 1
-#endif
-// The walks store the record offsets straight into the regions' lists in global memory instead of
-// an LDS list copied out afterwards (2 KiB less LDS per block).
-#ifndef PKTGPU_PCAP_GLIST
-#define PKTGPU_PCAP_GLIST 0
-#endif
 
 __device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, uint16_t* lst, uint64_t base, uint64_t entry,
                                            uint64_t len, bool valid, uint64_t& exit, uint32_t& cnt) {
@@ -505,11 +453,7 @@ __device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, u
         const uint32_t t = q + 16 + __builtin_elementwise_min(incl, room);            // < 2^32
         const bool over = act & (t > room);  // pkt_pcap_index: record runs past the end
         const bool rec = act & !over;
-        if constexpr (PKTGPU_PCAP_GLIST) {
-            if (rec) lst[c] = (uint16_t)q;  // straight to the region's list in global memory
-        } else {
-            lst[rec ? c : kMaxRec] = (uint16_t)q;
-        }
+        lst[act ? c : kMaxRec] = (uint16_t)q;  // (an overrunning record's start too: slot c, not counted)
         c += rec ? 1u : 0u;
         e |= over ? 1u : 0u;
         q = __builtin_elementwise_min(t, room);
@@ -532,29 +476,39 @@ __device__ __forceinline__ void lane_walk2(const uint32_t* lw, uint64_t lbase, u
 // (one region each, in parallel) instead of each on a whole wave: a walk is a serial chain of ~20
 // dependent hops whose ~20 VALU instructions per hop a wave issued for all 64 lanes — two thirds of
 // the kernel's VALU work (628 per wave, profiles/pcap/r03ad_pcap_guess_pmc.txt).
-#ifndef PKTGPU_PCAP_LANEWALK
-#define PKTGPU_PCAP_LANEWALK 1
-#endif
-#ifndef PKTGPU_PCAP_PERSIST
-#define PKTGPU_PCAP_PERSIST 0  // measured slower in every form: profiles/ab/r05o_pcap_guess_persistent.txt
-#endif
-// Issue priority of wave 0 while it walks the block's four regions (s_setprio; 0 = unchanged): the
-// other three waves of the block wait for the walks at the barrier, so a walk's hops should not queue
-// behind other blocks' candidate scans on the SIMD.
-#ifndef PKTGPU_PCAP_WALKPRIO
-#define PKTGPU_PCAP_WALKPRIO 0  // no effect measured (profiles/ab/r05p_pcap_walk_prio.txt)
-#endif
-#ifndef PKTGPU_PCAP_PREFETCH
-#define PKTGPU_PCAP_PREFETCH 1
-#endif
-#ifndef PKTGPU_PCAP_WPE
-#define PKTGPU_PCAP_WPE 0
-#endif
-#if PKTGPU_PCAP_WPE
-#define PCAP_PERSIST_WPE __attribute__((amdgpu_waves_per_eu(PKTGPU_PCAP_WPE, PKTGPU_PCAP_WPE)))
-#else
-#define PCAP_PERSIST_WPE
-#endif
+// Segment mode: the exact state before region r0 from the previous prefix's carry (B = its first
+// uncounted record start, C = its records): `entry` = region r0's exact entry, (last, cnt, bits) = the
+// exact state before it.  B inside region r0 (or later): its walk counts it.  B before region r0 (a
+// record that spanned the previous prefix's end, so the record after it starts past that end): the
+// record is counted here (rec_b: its index C, data at B + 16, incl_len b_incl) when it now ends inside
+// the prefix; when its header or its bytes still run past the end, nothing of the segment starts a
+// record (entry = last = len; kBitErr: the record runs past the end — an error unless partial).
+struct SegStart {
+    uint64_t entry, last, cnt;
+    uint32_t bits;
+    bool rec_b;
+    uint64_t b;
+    uint32_t b_incl;
+};
+__device__ __forceinline__ SegStart seg_start(const Scratch& S, const uint8_t* __restrict__ buf, uint64_t len) {
+    const uint64_t base = (uint64_t)S.r0 * kRegion, B = S.carry_in[kCarryB], C = S.carry_in[kCarryC];
+    SegStart r{B, B, C, 0u, false, B, 0u};
+    if (B >= base) return r;
+    r.entry = r.last = len;
+    if (B + 16 > len) return r;
+    const uint8_t* h = buf + B + 8;
+    const uint32_t incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
+    if (B + 16 + (uint64_t)incl > len) {
+        r.bits = kBitErr;
+        return r;
+    }
+    r.entry = r.last = B + 16 + (uint64_t)incl;
+    r.cnt = C + 1;
+    r.rec_b = true;
+    r.b_incl = incl;
+    return r;
+}
+
 // Diagnostic build only (-DPKTGPU_STAMPS=1, read by scripts/pcap_stamps.py): per wave of the guess
 // kernel, s_memrealtime at the start, after the staging barrier, after its candidate scan, after the
 // walk barrier and after its stores drained, + XCC id and the entry's distance from the region
@@ -581,58 +535,67 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
                                                          Scratch S) {
     constexpr uint32_t kStaged = kWaves * kRegion;
     __shared__ uint4 lds[kStaged / 16 + 2];
-    constexpr uint32_t kLst = PKTGPU_PCAP_GLIST ? 1 : kMaxRec + 2;  // + the dummy slot of lane_walk2
-    __shared__ uint16_t lst[kWaves][kLst];
+    __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
     __shared__ uint64_t s_entry[kWaves], s_exit[kWaves];
     __shared__ uint32_t s_cnt[kWaves];
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
-    const uint64_t lbase = (uint64_t)blockIdx.x * kStaged;
+    // (segment mode: the tiles start at region r0)
+    const uint32_t k0 = S.r0 + blockIdx.x * kWaves;
+    const uint64_t lbase = (uint64_t)k0 * kRegion;
+    const bool seg = S.carry_in != nullptr;
 #if PKTGPU_STAMPS
     uint64_t st_[5] = {0, 0, 0, 0, 0};
 #endif
     PCAP_STAMP(0);
+    if (blockIdx.x == 0 && t == 0 && S.carry_out) S.carry_out[kCarryB] = ~0ull;  // the scan's atomicMin target
     stage<kStaged, 256>(lds, buf, lbase, len, t);
     __syncthreads();
     PCAP_STAMP(1);
-    const uint32_t k = blockIdx.x * kWaves + w;
+    const uint32_t k = k0 + w;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     const uint64_t base = (uint64_t)k * kRegion;
-    if (PKTGPU_PCAP_LANEWALK && len - lbase <= 0xFFFFFFF0ull) {
+    // region 0 starts at 24 by definition; a segment's first region at the carry's exact entry
+    auto entry_of = [&]() -> uint64_t {
+        if (k >= K) return base + kRegion;
+        if (seg && k == S.r0) return seg_start(S, buf, len).entry;
+        if (!seg && k == 0) return 24;
+        return guess_entry<kStaged>(buf, len, lw, lbase, k);
+    };
+    if (len - lbase <= 0xFFFFFFF0ull) {
         // (lane_walk2 needs the file's end < 2 GiB past the staged bytes; lane_walk takes the rest)
-        const bool w2 = PKTGPU_PCAP_WALK2 && len - lbase <= 0x7FFFFFF0ull;
-        const uint64_t entry = k >= K ? base + kRegion : (k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k));
+        const bool w2 = len - lbase <= 0x7FFFFFF0ull;
+        const uint64_t entry = entry_of();
         PCAP_STAMP(2);
         if (lane == 0) s_entry[w] = entry;
         __syncthreads();
-        if (PKTGPU_PCAP_WALKPRIO && w == 0) __builtin_amdgcn_s_setprio(PKTGPU_PCAP_WALKPRIO);
         if (w == 0 && lane < (uint32_t)kWaves) {
-            const uint32_t kk = blockIdx.x * kWaves + lane;
+            const uint32_t kk = k0 + lane;
             const uint64_t en = s_entry[lane];
             uint64_t ex = 0;
             uint32_t cw = 0;
-            uint16_t* ll = PKTGPU_PCAP_GLIST ? S.list + (uint64_t)kk * kMaxRec : lst[lane];
+            uint16_t* ll = lst[lane];
             if (w2)
                 lane_walk2(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, kk < K, ex, cw);
             else if (kk < K)
                 lane_walk(lw, lbase, ll, (uint64_t)kk * kRegion, en, len, ex, cw);
-            if (S.partial) cw &= kCntMask;
             s_exit[lane] = ex;
             s_cnt[lane] = cw;
         }
-        if (PKTGPU_PCAP_WALKPRIO && w == 0) __builtin_amdgcn_s_setprio(0);
         __syncthreads();
         PCAP_STAMP(3);
         if (k >= K) return;
         const uint32_t cw = s_cnt[w], cnt = cw & kCntMask;
-        if constexpr (!PKTGPU_PCAP_GLIST) {
+        {
+            // the records' offsets + an overrunning record's start (slot cnt)
+            const uint32_t nl = cnt + ((cw & kCntErr) && cnt < kMaxRec ? 1u : 0u);
             uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
-            for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
+            for (uint32_t i = lane; i < nl; i += 64) dst[i] = lst[w][i];
         }
         if (lane == 0) {
             S.rentry[k] = entry;
             S.rexit[k] = s_exit[w];
             S.rcnt[k] = cw;
-            if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
+            if (!seg && k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
                 const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
                 __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
                 S.dev[1] = mg;
@@ -644,7 +607,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         if (lane == 0 && g_pcap_stamps) {
             uint32_t xcc;
             asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-            uint64_t* d = g_pcap_stamps + (uint64_t)k * 8u;
+            uint64_t* d = g_pcap_stamps + (uint64_t)(k - S.r0) * 8u;
             for (int q = 0; q < 5; q++) d[q] = st_[q];
             d[5] = xcc & 15u;
             d[6] = entry - base;
@@ -654,7 +617,7 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
         return;
     }
     if (k >= K) return;
-    const uint64_t entry = k == 0 ? 24 : guess_entry<kStaged>(buf, len, lw, lbase, k);
+    const uint64_t entry = entry_of();
     uint64_t exit;
     uint32_t cnt, err, rec;
     // (w = readfirstlane(t / 64), which lets the compiler see k as uniform and turn the walk into a
@@ -664,17 +627,16 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     // instructions, 736 -> 374 per wave, but each hop then waits ~3x longer: 80 vs 63 us per call,
     // profiles/ab/r03i_pcap_uniform_walk.txt)
     uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
-    walk(lw, lbase, PKTGPU_PCAP_GLIST ? dst : lst[w], base, entry, len, exit, cnt, err, rec);
-    if (S.partial) err = 0;
+    walk(lw, lbase, lst[w], base, entry, len, exit, cnt, err, rec);
     wave_lds_sync();
-    if (lane < cnt) dst[lane] = (uint16_t)rec;
-    if constexpr (!PKTGPU_PCAP_GLIST)
-        for (uint32_t i = 64 + lane; i < cnt; i += 64) dst[i] = lst[w][i];
+    const uint32_t nl = cnt + (err && cnt < kMaxRec ? 1u : 0u);  // + an overrunning record's start
+    if (lane < nl) dst[lane] = (uint16_t)rec;
+    for (uint32_t i = 64 + lane; i < nl; i += 64) dst[i] = lst[w][i];
     if (lane == 0) {
         S.rentry[k] = entry;
         S.rexit[k] = exit;
         S.rcnt[k] = cnt | (err ? kCntErr : 0u);
-        if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
+        if (!seg && k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
             const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
             __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             S.dev[1] = mg;
@@ -682,88 +644,13 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     }
 }
 
-// GUESS, persistent form (PKTGPU_PCAP_PERSIST): a grid the device holds at once, each block taking
-// tiles blockIdx.x, + gridDim.x, ... and loading its NEXT tile's 16 KiB into registers while it scans and
-// walks the current one, so a tile's memory latency (the one-shot kernel's staging: 1.64 us median,
-// p90 3.9 us of a 7 us wave, profiles/pcap/r05k_stamps.txt) hides behind the previous tile's LDS work;
-// the same per-tile work as pcap_guess_kernel's lane-walk path (files below 2 GiB: lane_walk2).
-constexpr uint32_t kGuessStaged = kWaves * kRegion;
-constexpr uint32_t kStagePieces = kGuessStaged / 16 + 2, kStagePer = (kStagePieces + 255) / 256;
-__device__ __forceinline__ void stage_load(uint4 (&v)[kStagePer], const uint8_t* buf, uint64_t base, uint64_t len,
-                                           uint32_t t) {
-#pragma unroll
-    for (uint32_t i = 0; i < kStagePer; i++) {
-        const uint32_t q = t + i * 256u;
-        const uint64_t a = base + 16ull * q;
-        v[i] = make_uint4(0, 0, 0, 0);
-        if (q <= kGuessStaged / 16 && a < len) v[i] = *reinterpret_cast<const uint4*>(buf + a);
-    }
-}
-__global__ __launch_bounds__(256) PCAP_PERSIST_WPE void pcap_guess_persist_kernel(const uint8_t* __restrict__ buf, uint64_t len,
-                                                                 uint32_t K, uint32_t ntiles, Scratch S) {
-    __shared__ uint4 lds[kStagePieces];
-    __shared__ uint16_t lst[kWaves][kMaxRec + 2];  // + the dummy slot of lane_walk2
-    __shared__ uint64_t s_entry[kWaves], s_exit[kWaves];
-    __shared__ uint32_t s_cnt[kWaves];
-    const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
-    const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
-    uint4 v[kStagePer];
-    uint32_t tile = blockIdx.x;
-    if (PKTGPU_PCAP_PREFETCH && tile < ntiles) stage_load(v, buf, (uint64_t)tile * kGuessStaged, len, t);
-    for (; tile < ntiles; tile += gridDim.x) {
-        const uint64_t lbase = (uint64_t)tile * kGuessStaged;
-        if (!PKTGPU_PCAP_PREFETCH) stage_load(v, buf, lbase, len, t);
-        __syncthreads();  // the previous tile's LDS reads are done
-#pragma unroll
-        for (uint32_t i = 0; i < kStagePer; i++)
-            if (t + i * 256u < kStagePieces) lds[t + i * 256u] = v[i];
-        __syncthreads();
-        // the next tile's bytes in flight while this one is scanned and walked
-        if (PKTGPU_PCAP_PREFETCH && tile + gridDim.x < ntiles)
-            stage_load(v, buf, (uint64_t)(tile + gridDim.x) * kGuessStaged, len, t);
-        const uint32_t k = tile * kWaves + w;
-        const uint64_t base = (uint64_t)k * kRegion;
-        const uint64_t entry = k >= K ? base + kRegion : (k == 0 ? 24 : guess_entry<kGuessStaged>(buf, len, lw, lbase, k));
-        if (lane == 0) s_entry[w] = entry;
-        __syncthreads();
-        if (w == 0 && lane < (uint32_t)kWaves) {
-            const uint32_t kk = tile * kWaves + lane;
-            uint64_t ex = 0;
-            uint32_t cw = 0;
-            lane_walk2(lw, lbase, lst[lane], (uint64_t)kk * kRegion, s_entry[lane], len, kk < K, ex, cw);
-            if (S.partial) cw &= kCntMask;
-            s_exit[lane] = ex;
-            s_cnt[lane] = cw;
-        }
-        __syncthreads();
-        if (k < K) {
-            const uint32_t cw = s_cnt[w], cnt = cw & kCntMask;
-            uint16_t* dst = S.list + (uint64_t)k * kMaxRec;
-            for (uint32_t i = lane; i < cnt; i += 64) dst[i] = lst[w][i];
-            if (lane == 0) {
-                S.rentry[k] = entry;
-                S.rexit[k] = s_exit[w];
-                S.rcnt[k] = cw;
-                if (k == 0) {  // pkt_pcap_index rejects a bad magic whatever follows
-                    const uint64_t mg = buf[0] == 0xD4 && buf[1] == 0xC3 && buf[2] == 0xB2 && buf[3] == 0xA1;
-                    __hip_atomic_store(&S.host[kHostMagic], mg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    S.dev[1] = mg;
-                }
-            }
-        }
-    }
-}
-
 // Block-wide exclusive composition of the threads' aggregates in thread order (all 256 threads).
 // Also returns `idx`: the thread index of the nearest claiming (non-none) aggregate before t, or -1.
-// The wave's inclusive scan by DPP moves (PKTGPU_PCAP_DPP): row_shr 1, 2, 4, 8 within each row of
+// The wave's inclusive scan by DPP moves: row_shr 1, 2, 4, 8 within each row of
 // 16 lanes, then row_bcast 15 and 31 across rows — register moves, no LDS; a lane without a source
 // takes the identity (update_dpp's `old`, bound_ctrl off), so every lane combines, without
 // divergence.  (The __shfl_up form below — ds_bpermute round trips, each step under `lane >= d` —
 // made the first block composition 2.8 us of every scan block, profiles/pcap/r04h2_stamps.txt.)
-#ifndef PKTGPU_PCAP_DPP
-#define PKTGPU_PCAP_DPP 1
-#endif
 template <int CTRL, int ROWS>
 __device__ __forceinline__ uint32_t dpp32(uint32_t old, uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROWS, 0xF, false);
@@ -805,28 +692,12 @@ __device__ __forceinline__ AggT<F> block_exclusive(AggT<F> a, int32_t& idx, AggT
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
     int32_t ix = (a.bits & kBitNone) ? -1 : (int32_t)t;
     AggT<F> x = a;
-    if constexpr (PKTGPU_PCAP_DPP) {
-        scan_step<0x111, 0xF>(x, ix);  // row_shr:1
-        scan_step<0x112, 0xF>(x, ix);  // row_shr:2
-        scan_step<0x114, 0xF>(x, ix);  // row_shr:4
-        scan_step<0x118, 0xF>(x, ix);  // row_shr:8
-        scan_step<0x142, 0xA>(x, ix);  // row_bcast:15 into rows 1 and 3
-        scan_step<0x143, 0xC>(x, ix);  // row_bcast:31 into rows 2 and 3
-    } else {
-#pragma unroll
-    for (uint32_t d = 1; d < 64; d <<= 1) {  // inclusive scan within the wave
-        AggT<F> y;
-        y.first = __shfl_up(x.first, d, 64);
-        y.last = __shfl_up(x.last, d, 64);
-        y.cnt = __shfl_up(x.cnt, d, 64);
-        y.bits = __shfl_up(x.bits, d, 64);
-        const int32_t iy = __shfl_up(ix, d, 64);
-        if (lane >= d) {
-            x = combine(y, x);
-            ix = ix >= 0 ? ix : iy;
-        }
-    }
-    }
+    scan_step<0x111, 0xF>(x, ix);  // row_shr:1
+    scan_step<0x112, 0xF>(x, ix);  // row_shr:2
+    scan_step<0x114, 0xF>(x, ix);  // row_shr:4
+    scan_step<0x118, 0xF>(x, ix);  // row_shr:8
+    scan_step<0x142, 0xA>(x, ix);  // row_bcast:15 into rows 1 and 3
+    scan_step<0x143, 0xC>(x, ix);  // row_bcast:31 into rows 2 and 3
     if (PKTGPU_STAMPS && bx) bx[0] = stamp_now();
     if (lane == 63) {
         wtot[w] = x;
@@ -852,25 +723,12 @@ __device__ __forceinline__ AggT<F> block_exclusive(AggT<F> a, int32_t& idx, AggT
     }
     total = run;
     // exclusive: the wave prefix before this lane
-    AggT<F> ex;
-    int32_t iex;
-    if constexpr (PKTGPU_PCAP_DPP) {  // wave_shr:1, lane 0 the identity
-        ex.first = dppf<0x138, 0xF, F>(0, x.first);
-        ex.last = dppf<0x138, 0xF, F>(0, x.last);
-        ex.cnt = dppf<0x138, 0xF, F>(0, x.cnt);
-        ex.bits = dpp32<0x138, 0xF>(kBitNone, x.bits);
-        iex = (int32_t)dpp32<0x138, 0xF>(0xFFFFFFFFu, (uint32_t)ix);
-    } else {
-        ex.first = __shfl_up(x.first, 1, 64);
-        ex.last = __shfl_up(x.last, 1, 64);
-        ex.cnt = __shfl_up(x.cnt, 1, 64);
-        ex.bits = __shfl_up(x.bits, 1, 64);
-        iex = __shfl_up(ix, 1, 64);
-        if (lane == 0) {
-            ex = agg_identity<F>();
-            iex = -1;
-        }
-    }
+    AggT<F> ex;  // wave_shr:1, lane 0 the identity
+    ex.first = dppf<0x138, 0xF, F>(0, x.first);
+    ex.last = dppf<0x138, 0xF, F>(0, x.last);
+    ex.cnt = dppf<0x138, 0xF, F>(0, x.cnt);
+    ex.bits = dpp32<0x138, 0xF>(kBitNone, x.bits);
+    const int32_t iex = (int32_t)dpp32<0x138, 0xF>(0xFFFFFFFFu, (uint32_t)ix);
     idx = iex >= 0 ? iex : ib;
     __syncthreads();  // wtot / widx reusable
     return combine(before, ex);
@@ -883,133 +741,13 @@ __device__ __forceinline__ bool seam_bad(const AggT<F>& pre, const AggT<F>& r) {
     return (r.bits & kBitNone) ? pre.last < r.last : pre.last != r.first;
 }
 
-#ifndef PKTGPU_PCAP_FIXWALK2
-#define PKTGPU_PCAP_FIXWALK2 1
-#endif
-#ifndef PKTGPU_PCAP_REUSE
-#define PKTGPU_PCAP_REUSE 1
-#endif
-// The scan blocks write the records after their look-back (no emit kernel).
-#ifndef PKTGPU_PCAP_SCANEMIT
-#define PKTGPU_PCAP_SCANEMIT 0  // measured slower: 82.1 vs 76.6 us per call (profiles/ab/r05q_pcap_scan_emit.txt)
-#endif
-#ifndef PKTGPU_PCAP_AGG0
-#define PKTGPU_PCAP_AGG0 1
-#endif
-#ifndef PKTGPU_PCAP_SPIN
-#define PKTGPU_PCAP_SPIN 1  // 78.1 vs 81.8-82.6 us per call (profiles/ab/r05m_pcap_lookback_spin.txt)
-#endif
-constexpr uint32_t kSpinMax = 4096;  // then the block-wide retry
-// The records, written by blocks of the scan kernel's own grid (PKTGPU_PCAP_COEMIT): blocks past the nb
-// scan blocks each take NR regions and wait — a relaxed agent-scope load per region, a short sleep between
-// tries — for the region words the scan blocks publish once their look-back is done: (record prefix << 1
-// | fixed), tagged with the call's epoch.  Then the wide emit over them (16-byte list loads issued before
-// the stores).  The records of a region its scan block re-walked are written by that block itself (their
-// list and exit were written in this kernel, by another CU); every other region's list, count and exit come
-// from the guess kernel, visible across the launch boundary.  Progress: the scan blocks have lower blockIdx,
-// so all of them are dispatched before any emit block, and none waits for an emit block.  This takes the
-// emit kernel's launch boundary off the call and overlaps its start with the scan (profiles/ab/r05v_*).
-#ifndef PKTGPU_PCAP_COEMIT
-#define PKTGPU_PCAP_COEMIT 0  // 0.3-0.9 us per call: not adopted (profiles/ab/r05v_pcap_coemit.txt)
-#endif
-constexpr uint32_t kCoEmitRegions = 64;
-#ifndef PKTGPU_PCAP_COEMIT_SLEEP
-#define PKTGPU_PCAP_COEMIT_SLEEP 12
-#endif
-constexpr uint32_t kCoEmitSpin = 1u << 22;
-__device__ __forceinline__ void coemit_block(uint32_t eb, uint32_t K, uint64_t cap, const Scratch& S,
-                                             uint64_t* __restrict__ offsets, uint32_t* __restrict__ lens,
-                                             const uint8_t* __restrict__ buf) {
-    constexpr uint32_t NR = kCoEmitRegions, PER = 4;
-    __shared__ uint64_t e_pre[NR + 1], e_ex[NR];
-    __shared__ uint32_t e_cpre[NR + 1], e_lastc;
-    __shared__ uint8_t e_fx[NR + 1];
-    const uint32_t t = threadIdx.x, k0 = eb * NR;
-    if (k0 >= K) return;
-    // one lane polls the last word the block needs (a scan block publishes its regions' words
-    // together), sleeping ~0.3 us between tries: 745 blocks x 65 polling lanes loaded the look-back's
-    // device-scope reads (profiles/ab/r05v_pcap_coemit.txt)
-    if (t == 0) {
-        const uint32_t kp = k0 + NR < K ? k0 + NR : K - 1;
-        for (uint32_t sp = 0; sp < kCoEmitSpin && tag_of(ld_agent(&S.rpre[kp])) != S.epoch; sp++)
-            __builtin_amdgcn_s_sleep(PKTGPU_PCAP_COEMIT_SLEEP);
-    }
-    __syncthreads();
-    if (t <= NR) {
-        const uint32_t k = k0 + t;
-        uint64_t pre = 0;
-        uint32_t fx = 0;
-        if (k < K) {
-            uint64_t pw = 0;
-            bool have = false;
-            for (uint32_t sp = 0;; sp++) {
-                pw = ld_agent(&S.rpre[k]);
-                if (tag_of(pw) == S.epoch) {
-                    have = true;
-                    break;
-                }
-                if (sp >= kCoEmitSpin) break;
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (!have)  // never expected: the call then reports an error instead of hanging
-                __hip_atomic_store(&S.host[kHostErr], (uint64_t)1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            pre = (pw & kValMask) >> 1;
-            fx = (uint32_t)(pw & 1u);
-            if (t < NR) e_ex[t] = S.rexit[k];
-            if (k == K - 1) e_lastc = fx ? 0u : (S.rcnt[k] & kCntMask);
-        }
-        e_pre[t] = pre;
-        e_fx[t] = (uint8_t)fx;
-    }
-    __syncthreads();
-    const uint64_t p0 = e_pre[0];
-    const uint64_t total = k0 + NR < K ? e_pre[NR] - p0 : e_pre[K - 1 - k0] + e_lastc - p0;
-    if (t <= NR) e_cpre[t] = k0 + t < K ? (uint32_t)(e_pre[t] - p0) : (uint32_t)total;
-    __syncthreads();
-    for (uint32_t i0 = 0; i0 < total && p0 + i0 < cap; i0 += 256u * PER) {
-        uint32_t rr[PER], li[PER], cc[PER], a[PER], b[PER];
-#pragma unroll
-        for (uint32_t u = 0; u < PER; u++) {
-            const uint32_t i = i0 + u * 256u + t;
-            uint32_t r = 0;
-#pragma unroll
-            for (uint32_t bb = NR / 2; bb; bb >>= 1)
-                if (e_cpre[r + bb] <= i) r += bb;
-            rr[u] = r;
-            li[u] = i - e_cpre[r];
-            cc[u] = e_cpre[r + 1] - e_cpre[r];
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PER; u++) {
-            const uint32_t i = i0 + u * 256u + t;
-            a[u] = b[u] = 0;
-            if (i < total && !e_fx[rr[u]]) {
-                const uint16_t* list = S.list + (uint64_t)(k0 + rr[u]) * kMaxRec;
-                a[u] = list[li[u]];
-                if (li[u] + 1 < cc[u]) b[u] = list[li[u] + 1];
-            }
-        }
-#pragma unroll
-        for (uint32_t u = 0; u < PER; u++) {
-            const uint32_t i = i0 + u * 256u + t;
-            const uint64_t idx = p0 + i;
-            if (i >= total || idx >= cap || e_fx[rr[u]]) continue;
-            const uint64_t base = (uint64_t)(k0 + rr[u]) * kRegion;
-            const uint64_t pos = base + a[u];
-            const bool last = li[u] + 1 == cc[u];
-            const uint64_t next = last ? e_ex[rr[u]] : base + b[u];
-            uint32_t incl = (uint32_t)(next - pos - 16);
-            if (S.partial && last) {  // a prefix of a capture: as pcap_emit_kernel
-                const uint8_t* h = buf + pos + 8;
-                incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
-            }
-            offsets[idx] = pos + 16;
-            lens[idx] = incl;
-        }
-    }
-}
+// The look-back: a lane whose block has published nothing yet re-reads it after a short sleep, up to
+// kSpinMax times, before the block-wide retry (78.1 vs 81.8-82.6 us per call without the spin,
+// profiles/ab/r05m_pcap_lookback_spin.txt).
+constexpr uint32_t kSpinMax = 4096;
 
-// Scan kernel (file header: SCAN).  Thread t = region blk * 256 + t.
+// Scan kernel (file header: SCAN).  Thread t = region r0 + blk * 256 + t.  (cap, offsets, lens: where a
+// segment's block 0 writes the record of the carry that spanned the previous prefix's end.)
 template <class F>
 __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restrict__ buf, uint64_t len, uint32_t K,
                                                         uint32_t nb, int ticket, Scratch S, uint64_t cap,
@@ -1022,10 +760,10 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     __shared__ uint32_t fq[kScanRegions];
     __shared__ uint64_t fe[kScanRegions];
     __shared__ uint8_t sbad[kScanRegions];
-    __shared__ uint8_t sfix[kScanRegions];  // re-walked in this kernel (PKTGPU_PCAP_COEMIT)
+    __shared__ uint16_t sov[kScanRegions];  // a walk that met a record running past the end: its start
     __shared__ Agg wtot[kWaves];
     __shared__ int32_t widx[kWaves];
-    __shared__ uint32_t s_blk, s_nf, s_retry, s_near, csum[kWaves];
+    __shared__ uint32_t s_blk, s_nf, s_retry, s_near;
     __shared__ Agg s_P;
     const uint32_t t = threadIdx.x, w = t / 64, lane = t & 63;
 #if PKTGPU_STAMPS
@@ -1034,10 +772,6 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     uint64_t t_bx = 0;  // after the first block composition
     uint64_t bx[2] = {0, 0};
 #endif
-    if (PKTGPU_PCAP_COEMIT && blockIdx.x >= nb) {  // an emit block (uniform)
-        coemit_block(blockIdx.x - nb, K, cap, S, offsets, lens, buf);
-        return;
-    }
     PCAP_STAMP(0);
     // the block order: blockIdx when the device could hold the whole grid at once (the host checks
     // the occupancy; progress then rests on the dispatcher launching workgroups in blockIdx order, so
@@ -1046,12 +780,15 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     if (t == 0) s_blk = ticket ? atomicAdd(S.ticket, 1u) : blockIdx.x;
     __syncthreads();
     const uint32_t blk = s_blk;
-    const uint32_t k = blk * kScanRegions + t;
-    sfix[t] = 0;
+    const bool seg = S.carry_in != nullptr;
+    const uint32_t k = S.r0 + blk * kScanRegions + t;
+    sov[t] = 0;
     if (k < K) {
         sen[t] = S.rentry[k];
         sex[t] = S.rexit[k];
-        scw[t] = S.rcnt[k];
+        const uint32_t cw = S.rcnt[k];
+        scw[t] = cw;
+        if (cw & kCntErr) sov[t] = S.list[(uint64_t)k * kMaxRec + (cw & kCntMask)];
     } else {
         sen[t] = sex[t] = 0;
         scw[t] = 0;
@@ -1063,12 +800,12 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     auto run_fixes = [&]() {
         const uint32_t nf = s_nf;
         for (uint32_t i = w; i < nf; i += kWaves) {
-            const uint32_t r = fq[i], kk = blk * kScanRegions + r;
+            const uint32_t r = fq[i], kk = S.r0 + blk * kScanRegions + r;
             const uint64_t base = (uint64_t)kk * kRegion, e = fe[i];
             wave_lds_sync();
             if (e < base + kRegion) stage<kRegion, 64>(lds[w], buf, base, len, lane);
             wave_lds_sync();
-            if (PKTGPU_PCAP_FIXWALK2 && len - base <= 0x7FFFFFF0ull) {  // wave-uniform
+            if (len - base <= 0x7FFFFFF0ull) {  // wave-uniform
                 // one lane walks (lane_walk2: the whole-wave walk below took ~9 us per fixed
                 // region, on the scan's critical path: profiles/pcap/r04q_stamps_guess_scan.txt)
                 uint64_t ex = 0;
@@ -1077,15 +814,14 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                     lane_walk2(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, true, ex, cw);
                 wave_lds_sync();
                 cw = (uint32_t)__shfl((int)cw, 0, 64);
-                if (S.partial) cw &= kCntMask;
                 ex = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex >> 32), 0, 64) << 32) |
                      (uint32_t)__shfl((int)(uint32_t)ex, 0, 64);
                 const uint32_t cnt = cw & kCntMask;
                 uint16_t* dst = S.list + (uint64_t)kk * kMaxRec;
                 for (uint32_t j = lane; j < cnt; j += 64) dst[j] = lst[w][j];
                 if (lane == 0) {
+                    sov[r] = (cw & kCntErr) ? lst[w][cnt] : 0;
                     sen[r] = e;
-                    sfix[r] = 1;
                     sex[r] = ex;
                     scw[r] = cw;
                     S.rentry[kk] = e;
@@ -1097,15 +833,16 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             uint64_t exit;
             uint32_t cnt, err, rec;
             walk(reinterpret_cast<const uint32_t*>(lds[w]), base, lst[w], base, e, len, exit, cnt, err, rec);
-            if (S.partial) err = 0;
             wave_lds_sync();
             uint16_t* dst = S.list + (uint64_t)kk * kMaxRec;
             if (lane < cnt) dst[lane] = (uint16_t)rec;
             for (uint32_t j = 64 + lane; j < cnt; j += 64) dst[j] = lst[w][j];
+            // an overrunning record's start: slot cnt (lane cnt's register below 64)
+            const uint32_t ov = (uint32_t)__shfl((int)rec, (int)(cnt & 63u), 64);
             if (lane == 0) {
                 const uint32_t cw = cnt | (err ? kCntErr : 0u);
+                sov[r] = err ? (uint16_t)(cnt < 64 ? ov : lst[w][cnt]) : 0;
                 sen[r] = e;
-                sfix[r] = 1;
                 sex[r] = exit;
                 scw[r] = cw;
                 S.rentry[kk] = e;
@@ -1174,8 +911,8 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             uint32_t st = 0;  // 0 unpublished, 1 aggregate, 2 exact
             Agg a = agg_identity<F>();
             uint64_t xl = 0, xc = 0, xm = 0;
-            // (PKTGPU_PCAP_SPIN: a lane whose block has published nothing yet re-reads it after a short
-            // sleep, up to kSpinMax times, instead of the whole window being re-read after a block-wide retry)
+            // (a lane whose block has published nothing yet re-reads it after a short sleep, up to
+            // kSpinMax times, instead of the whole window being re-read after a block-wide retry)
             for (uint32_t spin = 0; jj >= 0; spin++) {
                 // all seven fields in one round trip; a state counts only with the epoch in every field
                 const BlkDesc* d = S.blk + jj;
@@ -1195,14 +932,15 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
                     // definition; block 0 has no seam before it to fix): no wait for its exact
                     // state's publication, which a look-back's first read usually missed
                     // (one retry per block, ~2.5 us: profiles/pcap/r05k_stamps.txt)
-                    if (PKTGPU_PCAP_AGG0 && jj == 0 && !(a.bits & (kBitNone | kBitBad)) && a.first == 24) {
+                    // (not a segment's block 0: records before it are counted in the carry)
+                    if (!seg && jj == 0 && !(a.bits & (kBitNone | kBitBad)) && a.first == 24) {
                         st = 2;
                         xl = a.last;
                         xc = a.cnt;
                         xm = a.bits & kBitErr;
                     }
                 }
-                if (st || !PKTGPU_PCAP_SPIN || spin >= kSpinMax) break;
+                if (st || spin >= kSpinMax) break;
                 __builtin_amdgcn_s_sleep(1);
             }
             // the nearest exact block in the window (the smallest thread index with st == 2)
@@ -1259,6 +997,19 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         }
         if (blk == 0) {
             P = agg_identity<F>();
+            if (seg) {  // the exact state before region r0, from the carry
+                const SegStart ss = seg_start(S, buf, len);
+                P = mk_agg<F>(0, ss.last, ss.cnt, ss.bits);
+                if (t == 0) {
+                    if (ss.rec_b && ss.cnt - 1 < cap) {  // the spanning record, now whole
+                        offsets[ss.cnt - 1] = ss.b + 16;
+                        lens[ss.cnt - 1] = ss.b_incl;
+                    }
+                    // still not whole: it stays the next prefix's first uncounted record
+                    if (!ss.rec_b && ss.b < (uint64_t)S.r0 * kRegion && S.carry_out)
+                        atomicMin(reinterpret_cast<unsigned long long*>(&S.carry_out[kCarryB]), (unsigned long long)ss.b);
+                }
+            }
             break;
         }
         // P = the exact state before this block: (exit, count, error)
@@ -1279,10 +1030,13 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
     PCAP_STAMP(3);
     // ---- this block's seams against the exact exit before it: fix the first disagreeing region
     // from the exact state before it, until none disagrees (exact by induction)
-    Agg exact_pre = blk == 0 ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0);  // "claims" the exact exit
+    // (region 0 of a whole file has nothing before it; every other block, a segment's first included,
+    // has the exact state P before it)
+    const bool origin = blk == 0 && !seg;
+    Agg exact_pre = origin ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0);  // "claims" the exact exit
     // (the states have not changed since the local fixes' last composition: reuse it, and recompose
     // only after a fix below)
-    for (bool fresh = PKTGPU_PCAP_REUSE != 0;; fresh = false) {
+    for (bool fresh = true;; fresh = false) {
         const Agg mine = region_agg<F>(k, K, sen[t], sex[t], scw[t]);
         if (!fresh) {
             int32_t j;
@@ -1306,10 +1060,16 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
         run_fixes();
     }
     // ---- the exact state after this block; each region's record prefix
-    const Agg all = combine(blk == 0 ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0), total);
-    const uint64_t c_before = blk == 0 ? 0 : P.cnt;
+    const Agg all = combine(origin ? agg_identity<F>() : mk_agg<F>(P.last, P.last, 0, 0), total);
+    const uint64_t c_before = origin ? 0 : P.cnt;
     const uint32_t err_all = (P.bits | all.bits) & kBitErr;
     const uint64_t last = (all.bits & kBitNone) ? P.last : all.last;
+    // the carry: the first record start this prefix does not count — the start of the record that runs
+    // past its end, when the exact chain meets one (every region is now consistent, so a claiming region
+    // whose walk met one is on the chain), else the chain's exit; the smallest candidate wins
+    if (S.carry_out && k < K && (scw[t] & kCntErr) && !(sen[t] >= ((uint64_t)k + 1) * kRegion && k != 0))
+        atomicMin(reinterpret_cast<unsigned long long*>(&S.carry_out[kCarryB]),
+                  (unsigned long long)((uint64_t)k * kRegion + sov[t]));
     if (t == 0) {
         st_agent(&my->i_last, tagged(S.epoch, last));
         st_agent(&my->i_cnt, tagged(S.epoch, c_before + total.cnt));
@@ -1318,80 +1078,25 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
             // every block has taken its ticket by now (this one took the last): the next call's
             // tickets start at 0 without a memset launch on the call's critical path (4.7 us)
             if (ticket) st_agent(S.ticket, 0u);
+            // the magic check of region 0 (a segment: the first prefix's, carried)
+            const uint64_t magic = seg ? S.carry_in[kCarryMagic] : S.dev[1];
+            // a record running past the end is an error of the whole capture only (not of a prefix)
+            const bool err = err_all && !S.partial;
             __hip_atomic_store(&S.host[kHostTotal], c_before + total.cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&S.host[kHostMagic], magic, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
             // the count a parse on the same stream reads (kernel boundary: no fence needed); 0 when
             // the call fails (bad magic, a record past the end), so that parse writes nothing
-            *S.count_out = (S.dev[1] && !err_all) ? c_before + total.cnt : 0;
-            __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err_all ? 1 : 0), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_SYSTEM);
+            *S.count_out = (magic && !err) ? c_before + total.cnt : 0;
+            __hip_atomic_store(&S.host[kHostErr], (uint64_t)(err ? 1 : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            if (S.carry_out) {
+                S.carry_out[kCarryMagic] = magic;
+                atomicMin(reinterpret_cast<unsigned long long*>(&S.carry_out[kCarryB]), (unsigned long long)last);
+            }
         }
     }
     // each region's exact record prefix (the emit kernel writes the records): the records of the
     // regions before it in the block are the exclusive composition's count
-    if (PKTGPU_PCAP_SCANEMIT && PKTGPU_PCAP_REUSE) {
-        // the records themselves (no emit kernel): thread t writes region t's, from its list read 8
-        // entries (16 B) at a time — the next record's offset ends each one's incl_len, the region's
-        // exit ends its last (a prefix of a capture: the last one's header, as pcap_emit_kernel)
-        const uint32_t cnt = k < K ? (scw[t] & kCntMask) : 0u;
-        const uint64_t first = c_before + pre_cur.cnt, rbase = (uint64_t)k * kRegion, ex = sex[t];
-        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
-        for (uint32_t j0 = 0; j0 < cnt && first + j0 < cap; j0 += 8) {
-            const uint4 q = *reinterpret_cast<const uint4*>(list + j0);
-            const uint32_t nx = j0 + 8 < cnt ? list[j0 + 8] : 0u;
-            const uint32_t e[9] = {q.x & 0xFFFFu, q.x >> 16, q.y & 0xFFFFu, q.y >> 16, q.z & 0xFFFFu, q.z >> 16,
-                                   q.w & 0xFFFFu, q.w >> 16, nx};
-#pragma unroll
-            for (uint32_t u = 0; u < 8; u++) {
-                const uint32_t j = j0 + u;
-                if (j >= cnt || first + j >= cap) break;
-                const uint64_t pos = rbase + e[u];
-                const uint64_t next = j + 1 < cnt ? rbase + e[u + 1] : ex;
-                uint32_t incl = (uint32_t)(next - pos - 16);
-                if (S.partial && j + 1 == cnt) {
-                    const uint8_t* h = buf + pos + 8;
-                    incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
-                }
-                offsets[first + j] = pos + 16;
-                lens[first + j] = incl;
-            }
-        }
-    } else if (PKTGPU_PCAP_COEMIT && PKTGPU_PCAP_REUSE) {
-        if (k < K) {
-            const uint64_t first = c_before + pre_cur.cnt;
-            const bool fx = sfix[t] != 0;
-            if (fx && cap) {  // a region this block re-walked: its records from here (see coemit_block)
-                const uint32_t cnt = scw[t] & kCntMask;
-                const uint64_t rbase = (uint64_t)k * kRegion, ex = sex[t];
-                const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
-                for (uint32_t j = 0; j < cnt && first + j < cap; j++) {
-                    const uint64_t pos = rbase + list[j];
-                    const uint64_t next = j + 1 < cnt ? rbase + list[j + 1] : ex;
-                    uint32_t incl = (uint32_t)(next - pos - 16);
-                    if (S.partial && j + 1 == cnt) {
-                        const uint8_t* h = buf + pos + 8;
-                        incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
-                    }
-                    offsets[first + j] = pos + 16;
-                    lens[first + j] = incl;
-                }
-            }
-            st_agent(&S.rpre[k], tagged(S.epoch, (first << 1) | (fx ? 1u : 0u)));
-        }
-    } else if (PKTGPU_PCAP_REUSE) {
-        if (k < K) S.rpre[k] = c_before + pre_cur.cnt;
-    } else {
-        uint32_t x = k < K ? (scw[t] & kCntMask) : 0u, c = x;
-#pragma unroll
-        for (uint32_t d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= d) x += y;
-        }
-        if (lane == 63) csum[w] = x;
-        __syncthreads();
-        uint64_t before = c_before;
-        for (uint32_t q = 0; q < w; q++) before += csum[q];
-        if (k < K) S.rpre[k] = before + x - c;
-    }
+    if (k < K) S.rpre[k] = c_before + pre_cur.cnt;
 #if PKTGPU_STAMPS
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     PCAP_STAMP(4);
@@ -1407,60 +1112,10 @@ __global__ __launch_bounds__(256) void pcap_scan_kernel(const uint8_t* __restric
 #endif
 }
 
-// Emit (file header: EMIT): 256 threads write the records of 16 consecutive regions, one record per
-// thread per step, contiguous in the output (coalesced), at the regions' exact prefix.
-__global__ __launch_bounds__(256) void pcap_emit_kernel(uint32_t K, uint64_t cap, Scratch S,
-                                                        uint64_t* __restrict__ offsets,
-                                                        uint32_t* __restrict__ lens, const uint8_t* __restrict__ buf) {
-    __shared__ uint32_t cpre[kEmitRegions + 1];
-    __shared__ uint64_t cex[kEmitRegions];
-    const uint32_t k0 = blockIdx.x * kEmitRegions, t = threadIdx.x;
-    // every per-block value in one round trip: the block's first record index, the 16 regions'
-    // counts and exits (the exit ends each region's last record)
-    const uint64_t first = S.rpre[k0];
-    if (t < 64) {  // the 16 counts in parallel, prefix by a lane scan
-        const bool in = t < kEmitRegions && k0 + t < K;
-        const uint32_t c = in ? (S.rcnt[k0 + t] & kCntMask) : 0;
-        if (t < kEmitRegions) cex[t] = in ? S.rexit[k0 + t] : 0;
-        uint32_t x = c;
-#pragma unroll
-        for (uint32_t d = 1; d < kEmitRegions; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (t >= d) x += y;
-        }
-        if (t < kEmitRegions) cpre[t] = x - c;
-        if (t == kEmitRegions - 1) cpre[kEmitRegions] = x;
-    }
-    __syncthreads();
-    const uint32_t total = cpre[kEmitRegions];
-    for (uint32_t i = t; i < total; i += 256) {
-        const uint64_t idx = first + i;
-        if (idx >= cap) break;
-        uint32_t r = 0;
-#pragma unroll
-        for (uint32_t b = kEmitRegions / 2; b; b >>= 1)
-            if (cpre[r + b] <= i) r += b;
-        const uint32_t k = k0 + r, li = i - cpre[r], c = cpre[r + 1] - cpre[r];
-        const uint64_t base = (uint64_t)k * kRegion;
-        const uint16_t* list = S.list + (uint64_t)k * kMaxRec;
-        const uint64_t pos = base + list[li];
-        const uint64_t next = li + 1 < c ? base + list[li + 1] : cex[r];
-        offsets[idx] = pos + 16;
-        uint32_t incl = (uint32_t)(next - pos - 16);
-        if (S.partial && li + 1 == c) {
-            // a prefix of a capture: the walk that stopped at a record running past the prefix's end
-            // set its region's exit to that end, not to the record's start — the region's last counted
-            // record takes its incl_len from its own header (bytes pos + 8 .. pos + 11)
-            const uint8_t* h = buf + pos + 8;
-            incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
-        }
-        lens[idx] = incl;
-    }
-}
-
-// Emit, wider blocks (PKTGPU_PCAP_EMITR = NR regions per block, NR <= 64): every thread takes up to
-// PER records per pass and issues all their list loads before the first store, so a block waits one
-// round trip for its region words and one for its lists instead of one per record step.
+// Emit (file header: EMIT): NR consecutive regions per block; every thread takes up to PER records per
+// pass and issues all their list loads before the first store, so a block waits one round trip for its
+// region words and one for its lists instead of one per record step.  The records are contiguous in the
+// output (coalesced stores), at the regions' exact prefix.
 template <uint32_t NR, uint32_t PER>
 __global__ __launch_bounds__(256) void pcap_emit_wide_kernel(uint32_t K, uint64_t cap, Scratch S,
                                                              uint64_t* __restrict__ offsets,
@@ -1468,7 +1123,7 @@ __global__ __launch_bounds__(256) void pcap_emit_wide_kernel(uint32_t K, uint64_
     static_assert(NR >= 2 && NR <= 64 && (NR & (NR - 1)) == 0, "NR: a power of two <= 64");
     __shared__ uint32_t cpre[NR + 1];
     __shared__ uint64_t cex[NR];
-    const uint32_t k0 = blockIdx.x * NR, t = threadIdx.x;
+    const uint32_t k0 = S.r0 + blockIdx.x * NR, t = threadIdx.x;
     const uint64_t first = S.rpre[k0];
     if (t < 64) {
         const bool in = t < NR && k0 + t < K;
@@ -1518,7 +1173,10 @@ __global__ __launch_bounds__(256) void pcap_emit_wide_kernel(uint32_t K, uint64_
             const bool last = li[u] + 1 == cc[u];
             const uint64_t next = last ? cex[rr[u]] : base + b[u];
             uint32_t incl = (uint32_t)(next - pos - 16);
-            if (S.partial && last) {  // a prefix of a capture: as pcap_emit_kernel
+            if (S.partial && last) {
+                // a prefix of a capture: the walk that stopped at a record running past the prefix's end
+                // set its region's exit to that end, not to the record's start — the region's last
+                // counted record takes its incl_len from its own header (bytes pos + 8 .. pos + 11)
                 const uint8_t* h = buf + pos + 8;
                 incl = (uint32_t)h[0] | ((uint32_t)h[1] << 8) | ((uint32_t)h[2] << 16) | ((uint32_t)h[3] << 24);
             }
@@ -1570,7 +1228,8 @@ int pktgpu_pcap_reserve(pkt_ctx_t* ctx, uint64_t len, hipStream_t s) {
 // (Scratch.partial) and leave the record count in the device word count_out instead of the ctx's.
 static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
                        uint64_t cap, hipStream_t s, const uint64_t** count_dev, hipEvent_t* ev = nullptr,
-                       bool partial = false, uint64_t* count_out = nullptr) {
+                       bool partial = false, uint64_t* count_out = nullptr, uint32_t r0 = 0,
+                       const uint64_t* carry_in = nullptr, uint64_t* carry_out = nullptr) {
     if (!ctx || !buf || (cap && (!offsets || !lens))) return fail(ctx, PKT_ERR_INVALID_ARG, "bad argument");
     if (len < 24) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
     if (reinterpret_cast<uintptr_t>(buf) & 15) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap buffer not 16-byte aligned");
@@ -1578,7 +1237,9 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
         return fail(ctx, PKT_ERR_INVALID_ARG, "a queued capture's outcome has not been taken on this ctx (pkt_parse_pcap_result)");
     const uint64_t K64 = (len + kRegion - 1) / kRegion;
     if (K64 > (1ull << 31) || len >= kValMask) return fail(ctx, PKT_ERR_INVALID_ARG, "pcap too large");
-    const uint32_t K = (uint32_t)K64, nb = (K + kScanRegions - 1) / kScanRegions;
+    const uint32_t K = (uint32_t)K64;
+    if (r0 >= K || (r0 && !carry_in)) return fail(ctx, PKT_ERR_INVALID_ARG, "bad segment");
+    const uint32_t KS = K - r0, nb = (KS + kScanRegions - 1) / kScanRegions;  // the segment's regions [r0, K)
     hipError_t e = hipSetDevice(ctx->device);
     if (e != hipSuccess) return hip_fail(ctx, e, "hipSetDevice");
 
@@ -1618,23 +1279,14 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     S.count_out = count_out ? count_out : S.dev;
     S.epoch = pc.epoch;
     S.partial = partial ? 1u : 0u;
+    S.r0 = r0;
+    S.carry_in = carry_in;
+    S.carry_out = carry_out;
     for (int i = 0; i < kHostWords; i++) pc.ctl[i] = 0;
     const dim3 blk(256);
     if (ev && (e = hipEventRecord(ev[0], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
-    const uint32_t ntiles = (K + kWaves - 1) / kWaves;
-    if (PKTGPU_PCAP_PERSIST && !PKTGPU_STAMPS && len <= 0x7FFFFFF0ull) {
-        if (!pc.guess_resident) {  // guess blocks the device holds at once
-            int per_cu = 0, cus = 0;
-            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pcap_guess_persist_kernel, 256, 0) != hipSuccess ||
-                hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device) != hipSuccess)
-                per_cu = cus = 0;
-            pc.guess_resident = (uint32_t)std::max(1, per_cu * cus);
-        }
-        hipLaunchKernelGGL(pcap_guess_persist_kernel, dim3(std::min(ntiles, pc.guess_resident)), blk, 0, s, buf, len, K,
-                           ntiles, S);
-    } else {
-        hipLaunchKernelGGL(pcap_guess_kernel, dim3(ntiles), blk, 0, s, buf, len, K, S);
-    }
+    const uint32_t ntiles = (KS + kWaves - 1) / kWaves;
+    hipLaunchKernelGGL(pcap_guess_kernel, dim3(ntiles), blk, 0, s, buf, len, K, S);
     if (ev && (e = hipEventRecord(ev[1], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     if (!pc.scan_resident) {  // scan blocks the device holds at once
         int per_cu = 0, cus = 0;
@@ -1650,26 +1302,21 @@ static int pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_
     // such block has been dispatched (is resident or finished) — whatever else occupies the device,
     // e.g. the other ctx's capture of the async entries.  The occupancy test keeps the ticket for a
     // grid the device could not hold at once even alone.
-    const uint32_t ne = (PKTGPU_PCAP_COEMIT && cap) ? (K + kCoEmitRegions - 1) / kCoEmitRegions : 0u;
-    // 32-bit compositions while every position and count of the file fits (region ends included)
-    if (PKTGPU_PCAP_AGG32 && len + 2ull * kRegion < (1ull << 32))
-        hipLaunchKernelGGL(pcap_scan_kernel<uint32_t>, dim3(nb + ne), blk, 0, s, buf, len, K, nb,
+    // 32-bit compositions while every position and count of the file fits (region ends included), unless
+    // the ctx asks for the 64-bit ones (pkt_ctx_set_pcap_scan64: the form files past 4 GiB take)
+    if (!pc.scan64 && len + 2ull * kRegion < (1ull << 32))
+        hipLaunchKernelGGL(pcap_scan_kernel<uint32_t>, dim3(nb), blk, 0, s, buf, len, K, nb,
                            nb > pc.scan_resident ? 1 : 0, S, cap, offsets, lens);
     else
-        hipLaunchKernelGGL(pcap_scan_kernel<uint64_t>, dim3(nb + ne), blk, 0, s, buf, len, K, nb,
+        hipLaunchKernelGGL(pcap_scan_kernel<uint64_t>, dim3(nb), blk, 0, s, buf, len, K, nb,
                            nb > pc.scan_resident ? 1 : 0, S, cap, offsets, lens);
     if (ev && (e = hipEventRecord(ev[2], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     // (the records written by the scan blocks themselves, after their look-back, measured slower:
     // 36.9 vs 21.2 + 7.4 us per 2^20-record call — each of the 187 blocks walks its ~5.6K records with
     // a dependent global read per step, where the emit kernel's 3K blocks hide that latency, r04e)
-    if (cap && !PKTGPU_PCAP_SCANEMIT && !PKTGPU_PCAP_COEMIT) {
-        if constexpr (PKTGPU_PCAP_EMITR != 0)
-            hipLaunchKernelGGL((pcap_emit_wide_kernel<PKTGPU_PCAP_EMITR, PKTGPU_PCAP_EMITPER>),
-                               dim3((K + PKTGPU_PCAP_EMITR - 1) / PKTGPU_PCAP_EMITR), blk, 0, s, K, cap, S, offsets, lens, buf);
-        else
-            hipLaunchKernelGGL(pcap_emit_kernel, dim3((K + kEmitRegions - 1) / kEmitRegions), blk, 0, s, K, cap, S,
-                               offsets, lens, buf);
-    }
+    if (cap)
+        hipLaunchKernelGGL((pcap_emit_wide_kernel<kEmitRegions, kEmitPer>), dim3((KS + kEmitRegions - 1) / kEmitRegions), blk,
+                           0, s, K, cap, S, offsets, lens, buf);
     if (ev && (e = hipEventRecord(ev[3], s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     e = hipGetLastError();
     if (e != hipSuccess) return hip_fail(ctx, e, "pcap index launch");
@@ -1688,9 +1335,12 @@ static int pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) {
 }
 
 int pktgpu_pcap_launch(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, uint64_t* offsets, uint32_t* lens,
-                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, bool partial, uint64_t* count_out) {
-    return pcap_launch(ctx, buf, len, offsets, lens, cap, s, count_dev, nullptr, partial, count_out);
+                       uint64_t cap, hipStream_t s, const uint64_t** count_dev, bool partial, uint64_t* count_out,
+                       uint32_t r0, const uint64_t* carry_in, uint64_t* carry_out) {
+    return pcap_launch(ctx, buf, len, offsets, lens, cap, s, count_dev, nullptr, partial, count_out, r0, carry_in,
+                       carry_out);
 }
+uint32_t pktgpu_pcap_region_bytes() { return kRegion; }
 int pktgpu_pcap_finish(pkt_ctx_t* ctx, uint64_t* n_out) { return pcap_finish(ctx, n_out); }
 
 // The outcome of the capture queued on ctx (waits for it).

@@ -111,6 +111,10 @@ class Parser:
         """0 = auto, 1 = waterfall, 2 = lockstep (pkt_ctx_set_walk)."""
         self._check(self._L.pkt_ctx_set_walk(self._ctx, int(mode)), "pkt_ctx_set_walk")
 
+    def set_pcap_scan64(self, enable):
+        """pkt_ctx_set_pcap_scan64: the device pcap indexer's 64-bit compositions for every file."""
+        self._check(self._L.pkt_ctx_set_pcap_scan64(self._ctx, int(bool(enable))), "pkt_ctx_set_pcap_scan64")
+
     def set_host_piece(self, nbytes):
         """pkt_ctx_set_host_piece: bytes per copied piece of parse_pcap_host (0 = 16 MiB)."""
         self._check(self._L.pkt_ctx_set_host_piece(self._ctx, int(nbytes)), "pkt_ctx_set_host_piece")

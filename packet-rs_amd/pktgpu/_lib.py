@@ -69,6 +69,7 @@ SIGNATURES = {
     "pkt_ctx_set_staging": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_walk": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_ctx_set_host_piece": (ctypes.c_int, [_P, ctypes.c_uint64]),
+    "pkt_ctx_set_pcap_scan64": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_parse_batch": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_int,
                                        ctypes.POINTER(PktOut), _P]),
     "pkt_parse_batches": (ctypes.c_int, [_P, ctypes.POINTER(PktBatch), ctypes.c_uint32, ctypes.c_int,
@@ -138,6 +139,14 @@ SIGNATURES = {
     "pkt_mgpu_set_gather_rows": (ctypes.c_int, [_P, ctypes.c_int]),
     "pkt_shard_range": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_int, ctypes.c_int,
                                        ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64)]),
+    "pkt_pcap_stream_open": (ctypes.c_int, [ctypes.c_int, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int,
+                                            ctypes.POINTER(PktOut), ctypes.c_uint64, ctypes.POINTER(_P)]),
+    "pkt_pcap_stream_push": (ctypes.c_int, [_P, _P, ctypes.c_uint64]),
+    "pkt_pcap_stream_poll": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _P, _P]),
+    "pkt_pcap_stream_finish": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64), _P, _P]),
+    "pkt_pcap_stream_ctx": (_P, [_P]),
+    "pkt_pcap_stream_last_error": (ctypes.c_char_p, [_P]),
+    "pkt_pcap_stream_close": (ctypes.c_int, [_P]),
     "pkt_mgpu_create": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
     "pkt_mgpu_create_virtual": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.POINTER(_P)]),
     "pkt_mgpu_is_virtual": (ctypes.c_int, [_P]),

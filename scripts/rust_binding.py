@@ -17,7 +17,7 @@ C_SCALARS = {"uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": 
              "int": "c_int", "float": "f32", "size_t": "usize", "char": "c_char", "void": "c_void",
              "pkt_ctx_t": "PktCtx", "pkt_batch_t": "PktBatch", "pkt_out_t": "PktOut", "pkt_chain_t": "PktChain",
              "pkt_field_spec_t": "PktFieldSpec", "pkt_gen_field_t": "PktGenField", "pkt_gen_t": "PktGen",
-             "pkt_mgpu_t": "PktMgpu", "pkt_gather_piece_t": "PktGatherPiece"}
+             "pkt_mgpu_t": "PktMgpu", "pkt_gather_piece_t": "PktGatherPiece", "pkt_pcap_stream_t": "PktPcapStream"}
 STRUCTS = {"pkt_batch": "PktBatch", "pkt_out": "PktOut", "pkt_field_spec": "PktFieldSpec", "pkt_chain": "PktChain",
            "pkt_gen_field": "PktGenField", "pkt_gather_piece": "PktGatherPiece"}
 

@@ -344,3 +344,39 @@ def test_epoch_wrap_past_2_16_calls():
                 assert np.array_equal(o.cpu().numpy(), o_ref) and np.array_equal(l.cpu().numpy(), l_ref), call
     finally:
         Q.close()
+
+
+def test_scan64_composition_same_index():
+    """files under 4 GiB take the 32-bit scan compositions; pkt_ctx_set_pcap_scan64 forces
+    the 64-bit instantiation (the only one files >= 4 GiB run) so it stays pinned by the same captures:
+    the golden capture, fake chains, zero / large / empty records, random captures, a C4 replay, the
+    error cases, and a capture in HBM -> index -> parse == oracle."""
+    import pktgpu
+    import torch
+    Q = pktgpu.Parser(0)
+    try:
+        Q.set_pcap_scan64(True)
+        check_index(Q, open(os.path.join(GOLD, "ref22.pcap"), "rb").read(), "ref22 scan64")
+        test_fake_chains_in_payloads(Q)
+        test_zero_payloads_large_and_empty_records(Q)
+        test_random_captures(Q)
+        test_header_only_and_tails(Q)
+        test_errors_match_host(Q)
+        buf, offs, lens = gen.gen_c4(300_000, seed=64)
+        o, l, m = Q.pcap_index(dev(buf))
+        assert m == 300_000 and np.array_equal(o.cpu().numpy(), offs) and np.array_equal(l.cpu().numpy(), lens)
+        g = Q.parse(dev(buf), offsets=o, lens=l, columns="all")
+        torch.cuda.synchronize()
+        ref = oracle.parse_batch(buf, len(offs), offsets=offs, lens=lens, nthreads=8)
+        for k in ("status", "n_hdrs", "payload_off", "payload_len", "ipv4_csum_calc"):
+            assert np.array_equal(g[k].cpu().numpy(), ref[k]), k
+        Q.set_pcap_scan64(False)
+        check_index(Q, open(os.path.join(GOLD, "ref22.pcap"), "rb").read(), "ref22 scan32 again")
+    finally:
+        Q.close()
+    with pytest.raises(RuntimeError):
+        P_ = pktgpu.Parser(0)
+        try:
+            P_._check(P_._L.pkt_ctx_set_pcap_scan64(P_._ctx, 2), "pkt_ctx_set_pcap_scan64")
+        finally:
+            P_.close()

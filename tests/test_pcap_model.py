@@ -17,7 +17,7 @@ def u32(b, o):
         (bytes(b[o:o + 4]) + b"\0\0\0\0")[:4], "little")
 
 
-MIN_HOPS = 2  # PKTGPU_PCAP_HOPS (pktgpu_pcap.hip)
+MIN_HOPS = 2  # kMinHops (pktgpu_pcap.hip)
 MAX_HOPS = 2
 ORIG_MAX = 1 << 20
 TS_SPAN = 86400
@@ -70,7 +70,7 @@ def guess(b, k, snap):
     """First candidate of the region, 64 offsets per step: the lowest whose chain checks out in
     the tile's staged bytes (TILE regions + 16 B), else the lowest that checks out with reads past
     them, moved to the last of the run of consecutive verified candidates it starts, across steps
-    (PKTGPU_PCAP_RUNLAST);
+    (the run-last rule of guess_entry);
     none in the region -> "no record starts here"."""
     base = k * R
     stop = min(len(b), base + R)
