@@ -440,6 +440,33 @@ void parse_multi_kernel(MultiParams mp) {
     parse_block<NCH, GM, WK, L_MULTI>(p, blockIdx.x - b * mp.bpb, lds, T, pkt_st, b);
 }
 
+// The emit of one column group with its bases loaded from the kernel arguments right here (LATE): columns
+// [LO, HI) of pkt_out_t (group G), through an opaque copy of their address taken after a compiler memory
+// barrier, so the loads come after the previous group's stores.  One group's bases live at a time (at most
+// 13 pointers): the all-columns and C3 emits held every group's (~40 bases, 80 SGPRs) at once and spilled
+// 32-74 SGPRs to VGPR lanes (round-5 review).
+template <uint32_t GM, uint32_t G, int LO, int HI, int LATE, class View>
+__device__ __forceinline__ void emit_group_late(uint64_t kseg, int64_t delta, uint32_t i, uint32_t len, const View& pv,
+                                                const WalkResult& r) {
+    constexpr bool rt = (GM & G_RUNTIME) != 0;
+    if constexpr (rt || (GM & G) != 0) {
+        uint64_t ka = kseg + offsetof(KParams, out) + sizeof(void*) * LO;
+        asm volatile("" : "+s"(ka)::"memory");
+        const void* const KARG_AS* kc = reinterpret_cast<const void* const KARG_AS*>(ka);
+        pkt_out_t oc{};
+        void** ocp = reinterpret_cast<void**>(&oc);
+#pragma unroll
+        for (int c = LO; c < HI; c++) {
+            const void* q = kc[c - LO];
+            if constexpr (LATE == L_MULTI) q = q ? reinterpret_cast<const uint8_t*>(q) + delta : q;
+            ocp[c] = as_global(const_cast<void*>(q));
+        }
+        constexpr uint32_t GG = rt ? GM : (G | (GM & G_NT));
+        if constexpr (G == G_CHAIN) emit_chain<GG>(oc, i, len, r);
+        else emit_fields<GG>(oc, i, pv, r, r.status == PKT_OK);
+    }
+}
+
 template <int NCH, uint32_t GM, int WK, bool STAGED, int LATE>
 __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint32_t base,
                                            const u32x4 (&chunk)[NCH], uint64_t off_own, uint32_t len_own,
@@ -548,16 +575,15 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
                 asm volatile("" : "+s"(kd));
                 delta = *reinterpret_cast<const int64_t KARG_AS*>(kd);
             }
-            pkt_out_t oc;
-            void** ocp = reinterpret_cast<void**>(&oc);
-#pragma unroll
-            for (int c = 0; c < 49; c++) {
-                const void* q = kc[c];
-                if constexpr (LATE == L_MULTI) q = q ? reinterpret_cast<const uint8_t*>(q) + delta : q;
-                ocp[c] = as_global(const_cast<void*>(q));
-            }
-            emit_chain<GM>(oc, i_own, len_own, r);
-            emit_fields<GM>(oc, i_own, pv_own, r, r.status == PKT_OK);
+            (void)kc;
+            // column ranges of the groups in pkt_out_t order (group_masks)
+            emit_group_late<GM, G_CHAIN, 0, 7, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_ETHER, 7, 10, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_VLAN, 10, 14, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_IPV4, 14, 27, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_IPV6, 27, 35, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_TCP, 35, 45, LATE>(kseg, delta, i_own, len_own, pv_own, r);
+            emit_group_late<GM, G_UDP, 45, 49, LATE>(kseg, delta, i_own, len_own, pv_own, r);
         } else {
             emit_chain<GM>(out, i_own, len_own, r);
             emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
@@ -674,8 +700,16 @@ __global__ __launch_bounds__(kSpanBlock) void parse_span_kernel(KParams p) {
         if (lane == 0 && m) atomicMax(p.nh_max + (blockIdx.x & (kMaxSpread - 1)), m);
     }
     if (!active) return;
-    emit_chain<GM>(out, i, len, r);
-    emit_fields<GM>(out, i, pv, r, r.status == PKT_OK);
+    // the column bases group by group, loaded after the walk (parse_kernel's late loads: the kernel's
+    // only argument is the KParams, so the kernarg segment starts with it)
+    const uint64_t kseg = reinterpret_cast<uint64_t>(__builtin_amdgcn_kernarg_segment_ptr());
+    emit_group_late<GM, G_CHAIN, 0, 7, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_ETHER, 7, 10, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_VLAN, 10, 14, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_IPV4, 14, 27, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_IPV6, 27, 35, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_TCP, 35, 45, L_SINGLE>(kseg, 0, i, len, pv, r);
+    emit_group_late<GM, G_UDP, 45, 49, L_SINGLE>(kseg, 0, i, len, pv, r);
 }
 
 
@@ -917,7 +951,8 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         (void)hipFree(ctx->hp.pcarry);
         (void)hipFree(ctx->hp.pnh);
         (void)hipFree(ctx->hp.dcol);
-        if (ctx->hp.ev_copy) (void)hipEventDestroy(ctx->hp.ev_copy);
+        for (hipEvent_t x : ctx->hp.ev_copy)
+            if (x) (void)hipEventDestroy(x);
         if (ctx->hp.ev_parsed) (void)hipEventDestroy(ctx->hp.ev_parsed);
         for (hipEvent_t x : ctx->hp.ev_xdone)
             if (x) (void)hipEventDestroy(x);
@@ -1455,9 +1490,11 @@ struct Ingest {
     pkt_out_t dcols{};     // the parse's output: the caller's device columns or the ctx's hp.dcol
     bool exporting = false;
     ExportArgs xa{};       // exporting: hp.dcol -> the caller's pinned columns
-    uint64_t hi = 0;       // bytes copied to the device (hp.file[0, hi))
+    uint64_t hi = 0;       // bytes copied to the device (hp.file[0, hi)), queued
     uint64_t indexed = 0;  // the prefix the last step indexed
     uint64_t steps = 0;
+    uint64_t copies = 0;   // copies queued; copy c ends the capture's first copy_end[c % kCopyRing] bytes
+    uint64_t copy_end[HostPipe::kCopyRing] = {};
     int rc = PKT_SUCCESS;  // the first failure (every later call returns it)
 };
 constexpr uint64_t kHostPiece = 16ull << 20;  // pkt_parse_pcap_host: default bytes per copied piece
@@ -1516,7 +1553,7 @@ static int ingest_begin(Ingest& ig, pkt_ctx_t* ctx, uint64_t len_cap, uint64_t c
     ig.ctx = ctx;
     ig.entry = entry;
     ig.cap = cap;
-    ig.hi = ig.indexed = ig.steps = 0;
+    ig.hi = ig.indexed = ig.steps = ig.copies = 0;
     ig.rc = PKT_SUCCESS;
     int rc = pcap_host_buffers(ctx, len_cap, cap);
     if (rc != PKT_SUCCESS) return rc;
@@ -1524,7 +1561,8 @@ static int ingest_begin(Ingest& ig, pkt_ctx_t* ctx, uint64_t len_cap, uint64_t c
     hipError_t e = hipSuccess;
     if (!hp.pcarry) e = hipMalloc(reinterpret_cast<void**>(&hp.pcarry), HostPipe::kRing * kPcapCarryWords * 8);
     if (e == hipSuccess && !hp.pnh) e = hipMalloc(reinterpret_cast<void**>(&hp.pnh), HostPipe::kRing * kMaxSpread * 4);
-    if (e == hipSuccess && !hp.ev_copy) e = hipEventCreateWithFlags(&hp.ev_copy, hipEventDisableTiming);
+    for (int j = 0; j < HostPipe::kCopyRing && e == hipSuccess; j++)
+        if (!hp.ev_copy[j]) e = hipEventCreateWithFlags(&hp.ev_copy[j], hipEventDisableTiming);
     if (e == hipSuccess && !hp.ev_parsed) e = hipEventCreateWithFlags(&hp.ev_parsed, hipEventDisableTiming);
     for (int j = 0; j < HostPipe::kRing && e == hipSuccess; j++)
         if (!hp.ev_xdone[j]) e = hipEventCreateWithFlags(&hp.ev_xdone[j], hipEventDisableTiming);
@@ -1567,20 +1605,31 @@ static int ingest_begin(Ingest& ig, pkt_ctx_t* ctx, uint64_t len_cap, uint64_t c
 }
 
 // Copy the next n bytes of the capture in (hp.s[1], asynchronous: `src` must stay valid until the copy has
-// landed, hp.ev_copy).
+// landed, ingest_copied).
 static int ingest_copy(Ingest& ig, const uint8_t* src, uint64_t n) {
     if (ig.rc != PKT_SUCCESS) return ig.rc;
     HostPipe& hp = ig.ctx->hp;
+    const uint32_t c = (uint32_t)(ig.copies % HostPipe::kCopyRing);
     hipError_t e = hipMemcpyAsync(hp.file + ig.hi, src, n, hipMemcpyHostToDevice, hp.s[1]);
-    if (e == hipSuccess) e = hipEventRecord(hp.ev_copy, hp.s[1]);
+    if (e == hipSuccess) e = hipEventRecord(hp.ev_copy[c], hp.s[1]);
     if (e != hipSuccess) return ingest_fail(ig, hip_fail(ig.ctx, e, "hipMemcpyAsync H2D (capture bytes)"));
     ig.hi += n;
+    ig.copy_end[c] = ig.hi;
+    ig.copies++;
     return PKT_SUCCESS;
 }
 
-// One step over the bytes copied so far (last: the capture is complete — a record running past its end is
-// the capture's error; otherwise such a record waits for the next step).  Needs hi >= 24.
-static int ingest_step(Ingest& ig, bool last) {
+// The event of the queued copy that ends the first `upto` bytes (one of the last kCopyRing copies).
+static hipEvent_t ingest_copied(const Ingest& ig, uint64_t upto) {
+    for (uint64_t c = ig.copies; c > 0 && c + HostPipe::kCopyRing > ig.copies; c--)
+        if (ig.copy_end[(c - 1) % HostPipe::kCopyRing] == upto) return ig.ctx->hp.ev_copy[(c - 1) % HostPipe::kCopyRing];
+    return nullptr;
+}
+
+// One step over the first `upto` bytes (0: every byte copied so far; `upto` ends a queued copy among the
+// last kCopyRing) (last: the capture is complete — a record running past its end is the capture's error;
+// otherwise such a record waits for the next step).  Needs upto >= 24.
+static int ingest_step(Ingest& ig, bool last, uint64_t upto = 0) {
     if (ig.rc != PKT_SUCCESS) return ig.rc;
     pkt_ctx_t* ctx = ig.ctx;
     HostPipe& hp = ctx->hp;
@@ -1589,22 +1638,25 @@ static int ingest_step(Ingest& ig, bool last) {
     constexpr uint32_t R = HostPipe::kRing;
     const uint64_t k = ig.steps;
     const uint32_t j = (uint32_t)(k % R), jp = (uint32_t)((k + R - 1) % R);
-    const uint64_t region = pktgpu_pcap_region_bytes(), K = (ig.hi + region - 1) / region;
+    const uint64_t hi = upto ? upto : ig.hi;
+    const uint64_t region = pktgpu_pcap_region_bytes(), K = (hi + region - 1) / region;
     // the segment: from the region holding the previous step's end (its carry decides the exact entry),
     // at least the last region (a final step with no new bytes still decides the carried record)
     const uint32_t r0 = k ? (uint32_t)std::min<uint64_t>(ig.indexed / region, K - 1) : 0u;
-    hipError_t e = hipStreamWaitEvent(ps, hp.ev_copy, 0);
+    const hipEvent_t landed = ingest_copied(ig, hi);
+    if (!landed || hi < ig.indexed) return ingest_fail(ig, fail(ctx, PKT_ERR_INVALID_ARG, "capture step past its copies"));
+    hipError_t e = hipStreamWaitEvent(ps, landed, 0);
     // the ring slot this step writes was last read by step k - R + 1's export
     if (e == hipSuccess && ig.exporting && k + 1 >= R) e = hipStreamWaitEvent(ps, hp.ev_xdone[(k + 1) % R], 0);
     if (e != hipSuccess) return ingest_fail(ig, hip_fail(ctx, e, "hipStreamWaitEvent (capture step)"));
     uint64_t* carry = hp.pcarry + (uint64_t)j * kPcapCarryWords;
     const uint64_t* cin = k ? hp.pcarry + (uint64_t)jp * kPcapCarryWords : nullptr;
     const uint64_t* cnt = nullptr;
-    int rc = pktgpu_pcap_launch(ctx, hp.file, ig.hi, hp.ioffs, hp.ilens, ig.cap, ps, &cnt, !last, carry + 1, r0, cin, carry);
+    int rc = pktgpu_pcap_launch(ctx, hp.file, hi, hp.ioffs, hp.ilens, ig.cap, ps, &cnt, !last, carry + 1, r0, cin, carry);
     if (rc != PKT_SUCCESS) return ingest_fail(ig, rc);
     pkt_batch_t db;
     db.slab = hp.file;
-    db.slab_len = ig.hi;  // the prefix: every record parsed here lies inside it
+    db.slab_len = hi;  // the prefix: every record parsed here lies inside it
     db.offsets = hp.ioffs;
     db.lens = hp.ilens;
     db.stride = 0;
@@ -1615,7 +1667,7 @@ static int ingest_step(Ingest& ig, bool last) {
         return ingest_fail(ig, hip_fail(ctx, e, "hipMemsetAsync"));
     // the records this step added: [the previous step's count, this step's count)
     rc = parse_impl(ctx, &db, ig.entry, &ig.dcols, ps, 0, ctx->staging, nh, ig.cap, nullptr, cnt, cin ? cin + 1 : nullptr,
-                    (ig.hi - ig.indexed) / 16 + 1);
+                    (hi - ig.indexed) / 16 + 1);
     if (rc != PKT_SUCCESS) return ingest_fail(ig, rc);
     if (ig.exporting) {
         if ((e = hipEventRecord(hp.ev_parsed, ps)) != hipSuccess || (e = hipStreamWaitEvent(es, hp.ev_parsed, 0)) != hipSuccess)
@@ -1626,7 +1678,7 @@ static int ingest_step(Ingest& ig, bool last) {
         if ((e = pktgpu_export_launch(ig.xa, es)) != hipSuccess || (e = hipEventRecord(hp.ev_xdone[j], es)) != hipSuccess)
             return ingest_fail(ig, hip_fail(ctx, e, "export_kernel"));
     }
-    ig.indexed = ig.hi;
+    ig.indexed = hi;
     ig.steps++;
     return PKT_SUCCESS;
 }
@@ -1659,10 +1711,18 @@ static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, in
     Ingest ig;
     int rc = ingest_begin(ig, ctx, len, cap, entry, out, &hout);
     if (rc != PKT_SUCCESS) return rc;
-    for (uint64_t lo = 0; lo < len; lo += piece) {
-        const uint64_t hi = std::min(len, lo + piece);
-        if ((rc = ingest_copy(ig, buf + lo, hi - lo)) != PKT_SUCCESS) return rc;
-        if ((rc = ingest_step(ig, hi == len)) != PKT_SUCCESS) return rc;
+    // the copies run kAhead pieces ahead of the steps that wait for them (queued before the step's
+    // kernels on the host: a copy queued behind an export waited for that export's parse, r06e trace)
+    constexpr uint64_t kAhead = 3;
+    static_assert(kAhead < HostPipe::kCopyRing, "a step's copy is among the last kCopyRing");
+    const uint64_t np = (len + piece - 1) / piece;
+    for (uint64_t p = 0; p < np && p < kAhead; p++)
+        if ((rc = ingest_copy(ig, buf + p * piece, std::min(len, (p + 1) * piece) - p * piece)) != PKT_SUCCESS) return rc;
+    for (uint64_t p = 0; p < np; p++) {
+        const uint64_t q = p + kAhead;
+        if (q < np && (rc = ingest_copy(ig, buf + q * piece, std::min(len, (q + 1) * piece) - q * piece)) != PKT_SUCCESS)
+            return rc;
+        if ((rc = ingest_step(ig, p + 1 == np, std::min(len, (p + 1) * piece))) != PKT_SUCCESS) return rc;
     }
     if (!blocking) {
         ctx->pc.pending = true;
@@ -1791,7 +1851,8 @@ int pkt_pcap_stream_push(pkt_pcap_stream_t* st, const uint8_t* bytes, uint64_t n
     if (!n) return PKT_SUCCESS;
     int rc = ingest_copy(st->ig, bytes, n);
     // the caller may reuse its buffer once this returns
-    const hipError_t e = rc == PKT_SUCCESS ? hipEventSynchronize(st->ctx->hp.ev_copy) : hipSuccess;
+    const hipEvent_t landed = rc == PKT_SUCCESS ? ingest_copied(st->ig, st->ig.hi) : nullptr;
+    const hipError_t e = landed ? hipEventSynchronize(landed) : hipSuccess;
     if (e != hipSuccess) rc = ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventSynchronize (push)"));
     if (rc == PKT_SUCCESS && st->ig.hi >= 24 && st->ig.hi - st->ig.indexed >= st->step) rc = ingest_step(st->ig, false);
     return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);

@@ -30,7 +30,8 @@ struct HostPipe {
     static constexpr int kRing = 4;
     uint64_t* pcarry = nullptr;  // [kRing][4]
     uint32_t* pnh = nullptr;     // [kRing][256]: a step's n_hdrs maximum, spread
-    hipEvent_t ev_copy = nullptr;            // the bytes copied so far have landed
+    static constexpr int kCopyRing = 8;
+    hipEvent_t ev_copy[kCopyRing] = {};      // copy c has landed (slot c % kCopyRing)
     hipEvent_t ev_parsed = nullptr;          // the last step's records are parsed
     hipEvent_t ev_xdone[kRing] = {};         // step j's export has read its ring slot
     uint8_t* dcol = nullptr;     // the capture's columns on the device (the export's source)
