@@ -554,10 +554,11 @@ __global__ __launch_bounds__(256) void pcap_guess_kernel(const uint8_t* __restri
     const uint32_t k = k0 + w;
     const uint32_t* lw = reinterpret_cast<const uint32_t*>(lds);
     const uint64_t base = (uint64_t)k * kRegion;
-    // region 0 starts at 24 by definition; a segment's first region at the carry's exact entry
+    // region 0 starts at 24 by definition; a segment's first region is guessed like any other (the
+    // scan fixes it against the carry: reading the carry here cost the kernel 34 VGPRs, 8 -> 6 waves
+    // per SIMD, 50.9 -> 57.6 us per 2^20-record call)
     auto entry_of = [&]() -> uint64_t {
         if (k >= K) return base + kRegion;
-        if (seg && k == S.r0) return seg_start(S, buf, len).entry;
         if (!seg && k == 0) return 24;
         return guess_entry<kStaged>(buf, len, lw, lbase, k);
     };
