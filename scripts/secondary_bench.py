@@ -88,6 +88,44 @@ def event_ms(launch, iters, warm=3):
     return a.elapsed_time(b) / iters
 
 
+_PROBE = []
+
+
+def copy_ceiling(n, read_b, write_b, dev, it, kernel_ms):
+    """The no-work ceiling of a workload's byte shape (as the C2 line's
+    roofline.ceiling.stream_copy): libpktprobe's hand-written streaming copy reading read_b and writing
+    write_b bytes per packet (16-byte global_load/store_dwordx4 by consecutive lanes, 1 KiB contiguous
+    per wave instruction, 4 loads in flight per lane), one launch per batch over a >= 1 GiB ring, HIP
+    events on one stream.  `kernel_frac_of_copy` = copy time / the workload's kernel time."""
+    import ctypes
+    from bench import load_probe
+    if not _PROBE:
+        _PROBE.append(load_probe())
+    L = _PROBE[0]
+    if L is None:
+        return None
+    rb, wb = (int(read_b * n) + 15) // 16 * 16, (int(write_b * n) + 15) // 16 * 16
+    per = max(rb, wb, 16)
+    ring = max(2, (1 << 30) // per + 1)
+    srcs = [torch.empty(max(rb, 16), dtype=torch.uint8, device=dev) for _ in range(min(ring, 8))]
+    dsts = [torch.empty(max(wb, 16), dtype=torch.uint8, device=dev) for _ in range(ring)]
+    P8 = ctypes.POINTER(ctypes.c_uint8)
+    sp = [(P8 * 1)(ctypes.cast(ctypes.c_void_p(t.data_ptr()), P8)) for t in srcs]
+    dp = [(P8 * 1)(ctypes.cast(ctypes.c_void_p(t.data_ptr()), P8)) for t in dsts]
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+    def launch(k):
+        assert L.pkt_probe_stream_copy(sp[k % len(sp)], dp[k % ring], 1, rb, wb, st) == 0
+    ms = min(event_ms(launch, it) for _ in range(3))
+    del srcs, dsts
+    torch.cuda.empty_cache()
+    gbs = (rb + wb) / (ms * 1e-3) / 1e9
+    return {"kernel": "pkt_probe_stream_copy (libpktprobe.so): the workload's read and written bytes, contiguous, "
+                      "no work", "read_bytes": rb, "written_bytes": wb, "copy_us": round(ms * 1e3, 2),
+            "copy_frac_of_peak": round(gbs / PEAK, 4), "kernel_frac_of_copy": round(ms / kernel_ms, 4),
+            "measured": "min of 3 rounds of HIP events over back-to-back one-batch launches, same stream"}
+
+
 def line(name, n, ms, read_b, write_b, cpu, extra=None):
     gbs = (read_b + write_b) * n / (ms * 1e-3) / 1e9
     d = {"workload": name, "packets": n, "kernel_us": round(ms * 1e3, 2), "Gpkt/s": round(n / (ms * 1e-3) / 1e9, 3),
@@ -97,7 +135,14 @@ def line(name, n, ms, read_b, write_b, cpu, extra=None):
          "cpu_baseline": cpu}
     if extra:
         d.update(extra)
+    if CEILING[0]:
+        c = copy_ceiling(n, read_b, write_b, torch.device("cuda", 0), 20, ms)
+        if c is not None:
+            d["roofline"]["ceiling"] = c
     print(json.dumps(d), flush=True)
+
+
+CEILING = [True]
 
 
 def main():
@@ -106,7 +151,9 @@ def main():
     ap.add_argument("--iters", type=int, default=30)
     ap.add_argument("--cpu-budget", type=float, default=3.0)
     ap.add_argument("--only", default="")
+    ap.add_argument("--no-ceiling", action="store_true", help="skip the streaming-copy ceiling of each line")
     args = ap.parse_args()
+    CEILING[0] = not args.no_ceiling
     import oracle
     oracle.build()
     n, it = args.n, args.iters
