@@ -272,7 +272,8 @@ int         pkt_ctx_set_staging(pkt_ctx_t *ctx, int mode);
 int         pkt_ctx_set_walk(pkt_ctx_t *ctx, int mode);
 
 /* Tuning knob: bytes of file per copied piece of pkt_parse_pcap_host (pinned columns): 0 = the
- * default (16 MiB), else any value >= 4096.  Results are identical for every value. */
+ * default (16 MiB), else any value >= 4096; a capture is cut into at most 1024 pieces (larger pieces
+ * for files past 1024 x the knob).  Results are identical for every value. */
 int         pkt_ctx_set_host_piece(pkt_ctx_t *ctx, uint64_t bytes);
 
 /* Tuning / test knob: 1 = the device pcap indexer composes its regions' states in 64-bit positions

@@ -1711,6 +1711,11 @@ static int pcap_host_pieces(pkt_ctx_t* ctx, const uint8_t* buf, uint64_t len, in
     Ingest ig;
     int rc = ingest_begin(ig, ctx, len, cap, entry, out, &hout);
     if (rc != PKT_SUCCESS) return rc;
+    // at most kMaxHostSteps pieces per capture: each step costs ~50 us of host API time (13 calls), so
+    // tiny pieces over a large file would make the host the bottleneck (1 MiB pieces: 12.2 ms per 195 MB
+    // against 4.8 ms at 16 MiB, r06)
+    constexpr uint64_t kMaxHostSteps = 1024;
+    piece = std::max<uint64_t>(piece, (len + kMaxHostSteps - 1) / kMaxHostSteps);
     // the copies run kAhead pieces ahead of the steps that wait for them (queued before the step's
     // kernels on the host: a copy queued behind an export waited for that export's parse, r06e trace)
     constexpr uint64_t kAhead = 3;
