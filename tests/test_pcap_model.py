@@ -311,3 +311,154 @@ def test_model_prefixes_of_a_capture():
         o, l, _ = model_index(b[:cut], order_seed=i, block=4, partial=True,
                               inject={3: 3 * R + 1} if cut > 5 * R else None)
         assert np.array_equal(o, o_full[:m]) and np.array_equal(l, l_full[:m]), (cut, m, len(o))
+
+
+# ---------------------------------------------------------------------------- segment mode (round 6)
+def walk_ovr(b, base, entry):
+    """The round-6 walk: the error bit is kept in partial mode too (only the verdict ignores it) and the
+    start of the record that runs past the end is kept (the slot after the region's records)."""
+    pos, lst = entry, []
+    while pos < base + R and pos + 16 <= len(b):
+        incl = u32(b, pos + 8)
+        if pos + 16 + incl > len(b):
+            return len(b), lst, 1, pos
+        lst.append(pos)
+        pos += 16 + incl
+    return pos, lst, 0, None
+
+
+def seg_start(b, r0, carry):
+    """pktgpu_pcap.hip seg_start: (entry of region r0, exact exit before it, count before it, err, the
+    carried record (offset, incl) now counted or None, B kept as a carry candidate or None)."""
+    B, C = carry
+    base = r0 * R
+    if B >= base:
+        return B, B, C, False, None, None
+    n = len(b)
+    if B + 16 > n:
+        return n, n, C, False, None, B
+    incl = u32(b, B + 8)
+    if B + 16 + incl > n:
+        return n, n, C, True, None, B
+    return B + 16 + incl, B + 16 + incl, C + 1, False, (B + 16, incl), None
+
+
+def model_segment(b, r0, carry, partial, inject=None, order_seed=0, block=4):
+    """One step of the incremental index: regions [r0, K) of the prefix `b`, the exact state before
+    region r0 from `carry` = (B, C) of the previous step (None: the whole prefix from offset 24).
+    Returns (new records [(offset, incl)], the new carry (B', C'), error)."""
+    b = bytes(b)
+    snap = u32(b, 16) or (1 << 30)
+    K = (len(b) + R - 1) // R
+    seg = carry is not None
+    rng = np.random.default_rng(order_seed)
+    st = {}
+    for k in range(r0, K):  # the guess kernel guesses region r0 too (the scan fixes it against the carry)
+        e = 24 if (not seg and k == 0) else (inject or {}).get(k, guess(b, k, snap))
+        st[k] = (e, walk_ovr(b, k * R, e))
+
+    def agg(k):
+        e, (ex, lst, err, _) = st[k]
+        if k != 0 and e >= (k + 1) * R:
+            return ("none", (k + 1) * R)
+        return (e, ex, len(lst), bool(err), False)
+
+    ks = list(range(r0, K))
+    blocks = [ks[i:i + block] for i in range(0, len(ks), block)]
+    new = []
+    cands = []
+    if seg:
+        e0, E, C, err0, rec_b, keepB = seg_start(b, r0, carry)
+        if rec_b is not None:
+            new.append(rec_b)
+        if keepB is not None:
+            cands.append(keepB)
+    incl = []
+    for q, ks_q in enumerate(blocks):
+        if q == 0:
+            if seg:
+                pre0, cur = (E, E, 0, False, False), (E, C, err0)
+            else:
+                pre0, cur = IDENT, (24, 0, False)
+        else:
+            j = int(rng.integers(0, q))
+            acc = IDENT
+            for x in range(j + 1, q):
+                t = IDENT
+                for k in blocks[x]:
+                    t = combine(t, agg(k))
+                acc = combine(acc, t)
+            cur = incl[q - 1]
+            pre0 = (cur[0], cur[0], 0, False, False)
+        while True:  # fix the first disagreeing seam against the exact state, until none
+            pre, todo = pre0, None
+            for k in ks_q:
+                r = agg(k)
+                if seam_bad(pre, r) and not pre[4]:
+                    assert pre[1] >= k * R
+                    todo = (k, pre[1])
+                    break
+                pre = combine(pre, r)
+            if todo is None:
+                break
+            st[todo[0]] = (todo[1], walk_ovr(b, todo[0] * R, todo[1]))
+        tot = IDENT
+        for k in ks_q:
+            r = agg(k)
+            tot = combine(tot, r)
+            e, (ex, lst, err, ovr) = st[k]
+            if r[0] != "none" and err:  # a claiming region on the exact chain whose walk met an overrun
+                cands.append(ovr)
+        E_, C_, err_ = cur
+        incl.append((E_, C_, err_) if tot[0] == "none" else (tot[1], C_ + tot[2], err_ or tot[3]))
+    E_, C_, err_ = incl[-1]
+    cands.append(E_)
+    for k in ks:
+        _, (ex, lst, _, _) = st[k]
+        for i, p in enumerate(lst):
+            nxt = lst[i + 1] if i + 1 < len(lst) else ex
+            new.append((p + 16, u32(b, p + 8) if partial and i + 1 == len(lst) else nxt - p - 16))
+    assert len(new) == C_ - (carry[1] if seg else 0)
+    return new, (min(cands), C_), bool(err_) and not partial
+
+
+def test_model_segments_continue_from_the_carry():
+    """Round 6 (pktgpu_pcap.hip segment mode, pkt_pcap_stream_* / pkt_parse_pcap_host's pieces): a capture
+    indexed step by step — each step only the regions from the one holding the previous step's end, from
+    that step's carry (first uncounted record start, record count) — gives exactly the host indexer's
+    records over the whole capture, for random step ends (inside record headers, inside data, at
+    boundaries, one byte apart), long records spanning many steps, and wrong guesses injected into each
+    step's first region; a poll after each step sees exactly the records wholly inside the bytes so far."""
+    rng = np.random.default_rng(61)
+    pays = []
+    for i in range(700):
+        r = rng.random()
+        pays.append(bytes(int(rng.integers(5000, 14000))) if r < 0.08 else
+                    rng.integers(0, 256, int(rng.integers(1, 400)), dtype=np.uint8).tobytes())
+    caps = [records(pays, [(i, 0) for i in range(len(pays))]), gen.gen_c4(1500, seed=62)[0].tobytes()]
+    for ci, b in enumerate(caps):
+        o_full, l_full = gen.pcap_index_py(b)
+        ends = o_full.astype(np.int64) + l_full.astype(np.int64)
+        for trial in range(6):
+            cuts = sorted(set(int(x) for x in rng.integers(24, len(b), 10 + 4 * trial)))
+            cuts += [c + 1 for c in cuts[:3]]
+            cuts = sorted(set(c for c in cuts if c < len(b))) + [len(b)]
+            carry, prev, got = None, 0, []
+            for si, cut in enumerate(cuts):
+                K = (cut + R - 1) // R
+                r0 = 0 if carry is None else min(prev // R, K - 1)
+                inject = {r0: r0 * R + int(rng.integers(0, R))} if (trial % 2 and r0 > 0) else None
+                new, carry, err = model_segment(b[:cut], r0, carry, cut < len(b), inject=inject,
+                                                order_seed=trial * 100 + si, block=(2, 3, 5)[si % 3])
+                assert not err
+                got += new
+                m = int((ends <= cut).sum())
+                assert carry[1] == m, (ci, trial, cut, carry, m)
+                assert [x[0] for x in got] == [int(v) for v in o_full[:m]], (ci, trial, cut)
+                assert [x[1] for x in got] == [int(v) for v in l_full[:m]], (ci, trial, cut)
+                prev = cut
+    # the final step's verdict: a record running past the end of the capture is an error
+    b = caps[1]
+    _, carry, _ = model_segment(b[:len(b) // 2], 0, None, True)
+    _, _, err = model_segment(b[:-3], min((len(b) // 2) // R, (len(b) - 3 + R - 1) // R - 1), carry, False)
+    assert err
