@@ -576,21 +576,6 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
                 delta = *reinterpret_cast<const int64_t KARG_AS*>(kd);
             }
             (void)kc;
-#ifdef PKTGPU_AB_ONE_LOAD
-            if (true) {
-                pkt_out_t oc;
-                void** ocp = reinterpret_cast<void**>(&oc);
-#pragma unroll
-                for (int c = 0; c < 49; c++) {
-                    const void* q = kc[c];
-                    if constexpr (LATE == L_MULTI) q = q ? reinterpret_cast<const uint8_t*>(q) + delta : q;
-                    ocp[c] = as_global(const_cast<void*>(q));
-                }
-                emit_chain<GM>(oc, i_own, len_own, r);
-                emit_fields<GM>(oc, i_own, pv_own, r, r.status == PKT_OK);
-            } else
-#endif
-            {
             // column ranges of the groups in pkt_out_t order (group_masks)
             emit_group_late<GM, G_CHAIN, 0, 7, LATE>(kseg, delta, i_own, len_own, pv_own, r);
             emit_group_late<GM, G_ETHER, 7, 10, LATE>(kseg, delta, i_own, len_own, pv_own, r);
@@ -599,7 +584,6 @@ __device__ __forceinline__ void parse_tile(const KParams& p, uint8_t* lds, uint3
             emit_group_late<GM, G_IPV6, 27, 35, LATE>(kseg, delta, i_own, len_own, pv_own, r);
             emit_group_late<GM, G_TCP, 35, 45, LATE>(kseg, delta, i_own, len_own, pv_own, r);
             emit_group_late<GM, G_UDP, 45, 49, LATE>(kseg, delta, i_own, len_own, pv_own, r);
-            }
         } else {
             emit_chain<GM>(out, i_own, len_own, r);
             emit_fields<GM>(out, i_own, pv_own, r, r.status == PKT_OK);
