@@ -922,6 +922,12 @@ int pkt_ctx_destroy(pkt_ctx_t* ctx) {
         for (hipEvent_t ev : ctx->tv_ev)
             if (ev) (void)hipEventDestroy(ev);
     }
+    if (ctx && (ctx->tv_win || ctx->tv_win_ev)) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipDeviceSynchronize();
+        if (ctx->tv_win) (void)hipFree(ctx->tv_win);
+        if (ctx->tv_win_ev) (void)hipEventDestroy(ctx->tv_win_ev);
+    }
     if (ctx && ctx->mx.dev) {
         (void)hipSetDevice(ctx->device);
         (void)hipDeviceSynchronize();

@@ -102,9 +102,17 @@ struct pkt_ctx {
     // per call, so calls in flight on several streams do not share one; a word is reused only after
     // the call that last used it has passed its to_vec kernel (the call's stream waits on tv_ev[k])
     static constexpr uint32_t kTvFlags = 256;
+    static constexpr uint32_t kTvSlotWords = 8;  // a slot: the flag, then end(0) and end(n - 1) (u64, words 2-5)
     uint32_t* tv_flag = nullptr;
     hipEvent_t tv_ev[kTvFlags] = {};
     uint32_t tv_next = 0;
+    uint32_t tv_epoch = 0;  // the last call's mark (never 0: the words start zeroed)
+    // pkt_to_vec_batch in a capture's layout: per 4 KiB window of the slab, the first record ending
+    // past the window's start (one table per ctx; a call's stream waits on tv_win_ev, recorded after
+    // the previous call's window kernel, before writing it)
+    uint32_t* tv_win = nullptr;
+    uint64_t tv_win_cap = 0;
+    hipEvent_t tv_win_ev = nullptr;
     std::string err;
 };
 

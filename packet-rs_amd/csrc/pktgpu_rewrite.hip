@@ -14,6 +14,11 @@
 //                      (a wave scan of the per-packet counts) that the lanes copy 64 at a time
 //                      (a funnel shift when source and destination differ in alignment).  Q2
 //                      packets are gathered through the list by the whole wave, one at a time.
+//   tv_window_kernel   the same into a capture's own layout (records in order, none sharing a
+//                      16-byte chunk: tv_overlap_kernel checks on the device): one wave per 4 KiB of
+//                      destination, its source loads issued first, records found per chunk from a
+//                      map of the record starts in the window; chunks shared with the record
+//                      headers between records merged with the destination's own bytes.
 //   set_fields_kernel  set_bit_range (headers.rs:315-324) per spec, in spec order, in place; chain in
 //                      LDS, all specs (up to 32) in one launch.  The wave loads its packets' first 80
 //                      bytes into LDS cooperatively, every setter whose field lies there is applied in
@@ -275,28 +280,52 @@ struct TParams {
     uint64_t dst_len;
     const uint64_t* dst_offsets;
     uint32_t* out_len;
-    const uint32_t* overlap;  // PKTGPU_TOVEC_RMW: device word, 0 = no 16-byte chunk holds bytes of two records
+    // the window path (tv_window_kernel, below): *overlap == epoch when the batch is not for it
+    const uint32_t* overlap;  // device word (tv_overlap_kernel stores the call's epoch there)
+    uint32_t epoch;
+    bool win;                 // tv_window_kernel runs too: to_vec_kernel copies only when *overlap == epoch
 };
 
-// Edge chunks by read-modify-write (PKTGPU_TOVEC_RMW): in the input's own layout of an indexed
-// batch whose records are in order with no 16-byte chunk shared by two of them (a capture: the
-// 16-byte record headers lie between them), a packet's partial head / tail chunk is read from the
-// destination, its bytes merged in, and the chunk stored whole — one load and one 16-byte store
-// instead of up to eight dword / short / byte stores run by the whole wave for any lane's edge, and
-// the destination's bytes outside the packets are rewritten with their own values (no other lane
-// or wave touches that chunk).  tv_overlap_kernel decides per batch.
-#ifndef PKTGPU_TOVEC_RMW
-#define PKTGPU_TOVEC_RMW 1
-#endif
+// An indexed batch written into its own layout whose records are in order with no 16-byte chunk
+// shared by two of them (a capture: the 16-byte record headers lie between them) goes to
+// tv_window_kernel (below); tv_overlap_kernel decides per batch, on the device.
+constexpr uint32_t kTvWin = 4096;  // destination bytes per wave of tv_window_kernel
+
+constexpr uint64_t kTvMaxWin = 128;  // windows one record (+ the gap before it) may span (a pcap
+                                     // record is at most 256 KiB + 16 B: 65); more goes to to_vec_kernel
+
+// Does any 16-byte chunk hold bytes of two records (or a record lie out of order)?  One pass over
+// the index (12 B/record); if not, the pass also leaves tv_window_kernel's table: first[w] = the
+// first record ending past byte kTvWin * w, i.e. record i for the windows starting in
+// [end(i - 1), end(i)), written by pair (i - 1, i) (the windows before end(0) and from end(n - 1)
+// on are the window kernel's to know: both ends go beside the flag).  A record past the slab's end,
+// or one spanning more than kTvMaxWin windows, also sends the batch to to_vec_kernel.
 __global__ __launch_bounds__(256) void tv_overlap_kernel(const uint64_t* __restrict__ offs, const uint32_t* __restrict__ lens,
-                                                         uint64_t n, uint32_t* flag) {
-    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x + 1;  // pairs (i - 1, i)
+                                                         uint64_t n, uint32_t* flag, uint32_t epoch,
+                                                         uint32_t* __restrict__ first, uint64_t nwin, uint64_t slab_len) {
+    const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;  // pairs (i - 1, i)
     bool bad = false;
     if (i < n) {
-        const uint64_t o0 = offs[i - 1], l0 = lens[i - 1], o1 = offs[i];
-        bad = l0 == 0 || ((o0 + l0 - 1) >> 4) >= (o1 >> 4);
+        const uint64_t o1 = offs[i], e1 = o1 + lens[i];
+        bad = e1 > slab_len;
+        if (i == 0 || i == n - 1) reinterpret_cast<uint64_t*>(flag + 2)[i == 0 ? 0 : 1] = e1;
+        if (i >= 1) {
+            const uint64_t o0 = offs[i - 1], l0 = lens[i - 1], e0 = o0 + l0;
+            const bool pb = l0 == 0 || ((e0 - 1) >> 4) >= (o1 >> 4);
+            bad |= pb;
+            if (!pb) {
+                const uint64_t w0 = (e0 + kTvWin - 1) / kTvWin;
+                uint64_t w1 = (e1 + kTvWin - 1) / kTvWin;
+                w1 = w1 < nwin ? w1 : nwin;
+                if (w1 > w0 + kTvMaxWin) bad = true;
+                else
+                    for (uint64_t w = w0; w < w1; w++) first[w] = (uint32_t)i;
+            }
+        }
     }
-    if (__ballot(bad) && (threadIdx.x & 63u) == 0) atomicOr(flag, 1u);
+    // (a plain vector store of the call's epoch, no reset before the call: a word left by an
+    // older call holds another epoch)
+    if (__ballot(bad) && (threadIdx.x & 63u) == 0) __hip_atomic_store(flag, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // bytes [lo, hi) of the 16-byte chunk at ca from o, the rest from d (the destination's own bytes)
@@ -408,38 +437,65 @@ __device__ __forceinline__ void load_src_chunk(const BatchRef& b, uint64_t last1
 
 constexpr uint32_t kTvMapChunks = 2048;  // chunks per wave the start map covers (32 KiB of output)
 
+// Packet i's to_vec length and whether it is the packet's bytes [0, len) (ident); ok = parsed.
+__device__ __forceinline__ void tv_meta(const TParams& p, uint64_t i, uint32_t& ok, uint32_t& ident, uint32_t& len) {
+    // the four column reads issued together (no branch between them)
+    const uint32_t stt = p.status[i], po = p.payload_off[i], pl = p.payload_len[i];
+    const uint32_t hm = p.hdr_mask ? p.hdr_mask[i] : kGreOptMask;
+    ok = stt == PKT_OK;
+    ident = 1;
+    len = 0;
+    if (!ok) return;
+    // at most one GRE option type in the list: headers lie back to back in list order, so the
+    // list covers exactly [0, payload_off) and to_vec is the packet's bytes [0, len)
+    const bool sure = p.hdr_mask && __builtin_popcount(hm & kGreOptMask) <= 1;
+    uint32_t pos = po;
+    if (!sure) {
+        uint32_t nh = p.b.n_hdrs[i];
+        nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
+        pos = 0;
+        for (uint32_t j = 0; j < nh; j++) {  // identity iff every header sits where the list puts it
+            const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + i];
+            ident &= p.b.hdr_off[(uint64_t)j * p.b.n + i] == pos;
+            pos += ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
+        }
+        ident &= po == pos;
+    }
+    len = pos + pl;
+}
+
+// A Q2 packet (list order != wire order) by the whole wave: output byte q (lane q mod 64) comes
+// from the list entry covering it — header slices, then the payload.
+__device__ void tv_gather(const TParams& p, uint64_t ik, uint64_t s, uint64_t d, uint32_t L, uint32_t lane) {
+    uint32_t nh = p.b.n_hdrs[ik];
+    nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
+    for (uint32_t q = lane; q < L; q += 64u) {
+        uint32_t pos = 0, from = 0xFFFFFFFFu;
+        for (uint32_t j = 0; j < nh; j++) {
+            const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + ik];
+            const uint32_t sz = ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
+            if (from == 0xFFFFFFFFu && q < pos + sz) from = p.b.hdr_off[(uint64_t)j * p.b.n + ik] + (q - pos);
+            pos += sz;
+        }
+        if (from == 0xFFFFFFFFu) from = p.payload_off[ik] + (q - pos);
+        put_byte(p, d + q, p.b.slab[s + from]);
+    }
+}
+
 __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     const uint32_t lane = threadIdx.x & 63u;
     // wave-uniform values through readfirstlane (the compiler cannot tell threadIdx.x & ~63 is)
     const uint64_t base = ((uint64_t)blockIdx.x * kRwBlock +
                            __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u));  // wave's first packet
     const uint64_t i = base + lane;
+    if (p.win && __builtin_amdgcn_readfirstlane(*p.overlap) != p.epoch) return;  // tv_window_kernel copies
     // ---- per-lane metadata of packet i (coalesced column reads)
     uint64_t src = 0, dst = 0;
     uint32_t len = 0, ident = 1, ok = 0;
     if (i < p.b.n) {
-        ok = p.status[i] == PKT_OK;
         src = pkt_off(p.b, i);
         dst = p.dst_offsets ? p.dst_offsets[i] : src;
-        if (ok) {
-            const uint32_t po = p.payload_off[i], pl = p.payload_len[i];
-            // at most one GRE option type in the list: headers lie back to back in list order, so
-            // the list covers exactly [0, payload_off) and to_vec is the packet's bytes [0, len)
-            const bool sure = p.hdr_mask && __builtin_popcount(p.hdr_mask[i] & kGreOptMask) <= 1;
-            uint32_t pos = po;
-            if (!sure) {
-                uint32_t nh = p.b.n_hdrs[i];
-                nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
-                pos = 0;
-                for (uint32_t j = 0; j < nh; j++) {  // identity iff every header sits where the list puts it
-                    const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + i];
-                    ident &= p.b.hdr_off[(uint64_t)j * p.b.n + i] == pos;
-                    pos += ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
-                }
-                ident &= po == pos;
-            }
-            len = pos + pl;
-        }
+        tv_meta(p, i, ok, ident, len);
         if (p.out_len) p.out_len[i] = ok ? len : 0u;
     }
     // ---- identity packets: the wave's packets as ONE list of 16-byte destination chunks (a
@@ -514,9 +570,7 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     // 4 or 8 rounds' loads ahead was slower: C2 45 / 141 vs 33 us, C4 135 / 422 vs 125 us — 120+
     // VGPRs halve the resident waves, profiles/ab/r02tv_to_vec_unroll.txt.)
     uint32_t k = 0;
-    // uniform: edge chunks by read-modify-write (the batch's records never share a chunk)
-    const bool rmw = PKTGPU_TOVEC_RMW && p.overlap && __builtin_amdgcn_readfirstlane(*p.overlap) == 0;
-    auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4], uint32_t (&dd)[4]) {
+    auto locate = [&](uint32_t g, uint64_t& ca, uint64_t& lo, uint64_t& hi, uint32_t (&o)[4]) {
         uint64_t s, d;
         uint32_t L, pre;
         if (use_map) {  // rounds are located in order, each once
@@ -533,18 +587,9 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
         load_src_chunk(p.b, last16, s, d, ca, o);
         lo = ca > d ? ca : d;
         hi = ca + 16 < d + L ? ca + 16 : d + L;
-        if (rmw && !(lo == ca && hi == ca + 16) && ca + 16 <= p.dst_len) {  // the edge's own destination bytes
-            const uint4 v = *reinterpret_cast<const uint4*>(p.dst + ca);
-            dd[0] = v.x, dd[1] = v.y, dd[2] = v.z, dd[3] = v.w;
-        }
     };
-    auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4], uint32_t (&dd)[4]) {
-        if (rmw && !(lo == ca && hi == ca + 16) && ca + 16 <= p.dst_len) {
-            // (storing whole chunks through this same merged store too, one store per round: C4
-            // 143 vs 136 us, packed and C2 slower as well: profiles/ab/r04z_to_vec_rmw_edges.txt)
-            merge_chunk(ca, lo, hi, o, dd);
-            *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(dd[0], dd[1], dd[2], dd[3]);
-        } else if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
+    auto put = [&](uint64_t ca, uint64_t lo, uint64_t hi, const uint32_t (&o)[4]) {
+        if (lo == ca && hi == ca + 16 && ca + 16 <= p.dst_len) {
             if (dense) {
                 typedef uint32_t v4u __attribute__((ext_vector_type(4)));
                 __builtin_nontemporal_store(v4u{o[0], o[1], o[2], o[3]}, reinterpret_cast<v4u*>(p.dst + ca));
@@ -558,44 +603,174 @@ __global__ __launch_bounds__(kRwBlock) void to_vec_kernel(TParams p) {
     if (total <= 4u * 64u) {  // short waves (C2: 4 rounds): the plain loop is faster (33.7 vs 34.4 us)
         for (uint32_t g = lane; g < total; g += 64u) {
             uint64_t ca, lo, hi;
-            uint32_t o[4], dd[4] = {0, 0, 0, 0};
-            locate(g, ca, lo, hi, o, dd);
-            put(ca, lo, hi, o, dd);
+            uint32_t o[4];
+            locate(g, ca, lo, hi, o);
+            put(ca, lo, hi, o);
         }
     } else {  // C4: 142 vs 148 us in the input's layout, 124 vs 138 us packed (two rounds ahead:
               // 141 / 108 vs 142 / 105 us, round 3, profiles/ab/r03g_to_vec_lookahead2.txt)
         uint64_t ca = 0, lo = 0, hi = 0;
-        uint32_t o[4] = {0, 0, 0, 0}, dd[4] = {0, 0, 0, 0};
-        locate(lane, ca, lo, hi, o, dd);  // lane < 256 < total
+        uint32_t o[4] = {0, 0, 0, 0};
+        locate(lane, ca, lo, hi, o);  // lane < 256 < total
         for (uint32_t g = lane; g < total; g += 64u) {
             uint64_t ca1 = 0, lo1 = 0, hi1 = 0;
-            uint32_t o1[4] = {0, 0, 0, 0}, dd1[4] = {0, 0, 0, 0};
-            if (g + 64u < total) locate(g + 64u, ca1, lo1, hi1, o1, dd1);
-            put(ca, lo, hi, o, dd);
+            uint32_t o1[4] = {0, 0, 0, 0};
+            if (g + 64u < total) locate(g + 64u, ca1, lo1, hi1, o1);
+            put(ca, lo, hi, o);
             ca = ca1, lo = lo1, hi = hi1;
             o[0] = o1[0], o[1] = o1[1], o[2] = o1[2], o[3] = o1[3];
-            dd[0] = dd1[0], dd[1] = dd1[1], dd[2] = dd1[2], dd[3] = dd1[3];
         }
     }
     // ---- Q2 packets (two or more GRE options), one at a time by the whole wave: output byte q
     // (lane q mod 64) comes from the list entry covering it — header slices, then the payload
     for (uint64_t q2 = __ballot(ok && !ident); q2; q2 &= q2 - 1) {  // uniform
         const uint32_t kk = (uint32_t)__builtin_ctzll(q2);
-        const uint64_t ik = base + kk, s = s_src[w][kk], d = s_dst[w][kk];
-        const uint32_t L = s_len[w][kk];
-        uint32_t nh = p.b.n_hdrs[ik];
-        nh = nh > PKT_MAX_HDRS ? PKT_MAX_HDRS : nh;
-        for (uint32_t q = lane; q < L; q += 64u) {
-            uint32_t pos = 0, from = 0xFFFFFFFFu;
-            for (uint32_t j = 0; j < nh; j++) {
-                const uint32_t ty = p.b.hdr_type[(uint64_t)j * p.b.n + ik];
-                const uint32_t sz = ty < PKT_HDR_COUNT ? kHdrSize[ty] : 0;
-                if (from == 0xFFFFFFFFu && q < pos + sz) from = p.b.hdr_off[(uint64_t)j * p.b.n + ik] + (q - pos);
-                pos += sz;
+        tv_gather(p, base + kk, s_src[w][kk], s_dst[w][kk], s_len[w][kk], lane);
+    }
+}
+
+// ---- to_vec in a capture's own layout, by destination window.  An indexed batch written to
+// dst_offsets == its own offsets whose records are in order with no 16-byte chunk holding bytes of
+// two of them (tv_overlap_kernel: a capture, whose 16-byte record headers lie between the records)
+// is copied as the slab itself: wave w owns destination bytes [4096 w, 4096 (w + 1)) — 256 chunks,
+// four per lane (chunks lane, lane + 64, ..), all four loads in flight before the first store —
+// and finds which record owns each chunk from a 256-bit map of the record starts in the window
+// (rank = starts at or below the chunk, as in to_vec_kernel's map).  Every chunk with bytes of a
+// copied record is one 16-byte store: whole chunks straight from the source, the chunks a record
+// shares with the record headers beside it merged with the destination's own bytes (no other
+// wave holds that chunk).  Where to_vec_kernel gives each wave 64 records' chunks as a chain of
+// dependent rounds (~13 per wave at C4), here each wave has one round of independent loads.
+// first[w] = the first record ending past byte 4096 w (tv_overlap_kernel); records starting in
+// the window write out_len; a Q2 record (list order != wire order) is gathered byte by byte by the
+// wave holding its start.
+constexpr uint32_t kTvWinWords = kTvWin / 16 / 64;  // 64-bit words of the start map
+
+__global__ __launch_bounds__(kRwBlock) void tv_window_kernel(TParams p, const uint32_t* __restrict__ first,
+                                                             uint64_t nwin) {
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint64_t w = (uint64_t)blockIdx.x * (kRwBlock / 64) + wv;
+    if (w >= nwin) return;
+    __shared__ uint64_t s_map[kRwBlock / 64][kTvWinWords];
+    __shared__ uint64_t s_o[kRwBlock / 64][64];
+    __shared__ uint32_t s_l[kRwBlock / 64][64];
+    const uint64_t wa = w * kTvWin, we = wa + kTvWin;
+    const uint64_t last16 = ((p.b.slab_len + 15) & ~(uint64_t)15) - 16;
+    // The window's source chunks need nothing but w (the destination is the source's layout):
+    // their loads go first, in flight through the whole lookup below (a chunk outside every copied
+    // record loads and drops its bytes; past the slab, the last chunk again).
+    uint32_t sv[kTvWinWords][4];
+#pragma unroll
+    for (uint32_t q = 0; q < kTvWinWords; q++) {
+        uint64_t a = wa + 16u * (64u * q + lane);
+        a = a > last16 ? last16 : a;
+        const uint4 v = *reinterpret_cast<const uint4*>(p.b.slab + a);
+        sv[q][0] = v.x, sv[q][1] = v.y, sv[q][2] = v.z, sv[q][3] = v.w;
+    }
+    // the flag, end(0) and end(n - 1) (tv_overlap_kernel, same slot) and the window's table entry
+    // in one round trip (first[w] is unset, and not used, for the windows before end(0))
+    const uint64_t* ends = reinterpret_cast<const uint64_t*>(p.overlap + 2);
+    const uint32_t flag = *p.overlap, fw = first[w];
+    const uint64_t e0 = ends[0], en = ends[1];
+    asm volatile("" ::"s"(flag), "s"(fw), "s"(e0), "s"(en));  // (keeps the four loads ahead of the branches)
+    if (flag == p.epoch) return;  // records share chunks: to_vec_kernel
+    // (every record lies inside the slab: tv_overlap_kernel)
+    if (wa >= en) return;  // past the last record
+    uint64_t i0 = wa < e0 ? 0u : fw;
+    // 64 records at a time while they start inside the window: the first batch straight-line (a
+    // loop header would wait for the source loads above), the rare further ones in a loop
+    auto batch = [&](uint64_t i0) __attribute__((always_inline)) -> bool {
+        const uint64_t i = i0 + lane;
+        uint64_t o = ~0ull;
+        uint32_t len = 0, md = 0;  // md: 1 = copied by chunks, 2 = gathered (Q2)
+        bool sin = false;
+        if (i < p.b.n) {
+            // the record's start and its columns read together (those of records starting past
+            // the window too: one round trip, not two)
+            o = p.b.offsets[i];
+            uint32_t ok = 0, ident = 1;
+            tv_meta(p, i, ok, ident, len);
+            if (o < we) {
+                md = ok && len ? (ident ? 1u : 2u) : 0u;
+                sin = o >= wa;
+            } else {
+                len = 0;
             }
-            if (from == 0xFFFFFFFFu) from = p.payload_off[ik] + (q - pos);
-            put_byte(p, d + q, p.b.slab[s + from]);
         }
+        if (lane < kTvWinWords) s_map[wv][lane] = 0;
+        s_o[wv][lane] = o;
+        s_l[wv][lane] = len | md << 30;  // len <= 2 * 65535
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const bool st = sin && o < we;  // starts at chunk (o - wa) / 16 of this window
+        if (st) {
+            const uint32_t g = (uint32_t)((o - wa) >> 4);
+            atomicOr(reinterpret_cast<uint32_t*>(s_map[wv]) + (g >> 5), 1u << (g & 31u));
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        // chunk g's record: lane (starts at or below g) - s0, s0 = 1 when the batch's first record
+        // starts in the window (chunks before it are not the batch's), else it began before
+        const uint32_t s0 = (uint32_t)(__ballot(st) & 1ull);
+        uint32_t run = 0;
+        uint32_t az[kTvWinWords];  // the record's bytes [a, z) of chunk q (a | z << 8; 0 = none)
+        uint32_t dv[kTvWinWords][4];
+#pragma unroll
+        for (uint32_t q = 0; q < kTvWinWords; q++) {
+            const uint64_t word = s_map[wv][q];
+            const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(word >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)word, 0u));
+            const int32_t r = (int32_t)(run + below + (uint32_t)((word >> lane) & 1u)) - (int32_t)s0;
+            run += (uint32_t)__builtin_popcountll(word);
+            const uint64_t ca = wa + 16u * (64u * q + lane);
+            az[q] = 0;
+            if (r >= 0 && r < 64) {
+                const uint64_t ro = s_o[wv][r];
+                const uint32_t rl = s_l[wv][r];
+                if ((rl >> 30) == 1u) {
+                    const uint64_t re = ro + (rl & 0x3FFFFFFFu);
+                    const uint64_t lo = ca > ro ? ca : ro, hi = ca + 16 < re ? ca + 16 : re;
+                    if (lo < hi) az[q] = (uint32_t)(lo - ca) | (uint32_t)(hi - ca) << 8;
+                }
+            }
+            // unconditional (no branch joins a loaded value: a join would wait for it, the
+            // chunks' loads going one at a time): a chunk that is not an edge reloads its
+            // source (same address: no new HBM traffic)
+            const uint64_t a = ca > last16 ? last16 : ca;
+            const uint8_t* dp = az[q] && az[q] != (16u << 8) && ca + 16 <= p.dst_len ? p.dst + ca : p.b.slab + a;
+            const uint4 u = *reinterpret_cast<const uint4*>(dp);
+            dv[q][0] = u.x, dv[q][1] = u.y, dv[q][2] = u.z, dv[q][3] = u.w;
+        }
+#pragma unroll
+        for (uint32_t q = 0; q < kTvWinWords; q++) {
+            if (!az[q]) continue;
+            const uint64_t ca = wa + 16u * (64u * q + lane);
+            const uint64_t lo = ca + (az[q] & 0xFFu), hi = ca + (az[q] >> 8);
+            if (ca + 16 > p.dst_len) {  // the destination's last partial chunk
+                for (uint64_t x = lo; x < hi; x++) put_byte(p, x, sv[q][(x - ca) >> 2] >> (8 * (x & 3)));
+            } else if (az[q] == (16u << 8)) {
+                typedef uint32_t v4u __attribute__((ext_vector_type(4)));
+                __builtin_nontemporal_store(v4u{sv[q][0], sv[q][1], sv[q][2], sv[q][3]}, reinterpret_cast<v4u*>(p.dst + ca));
+            } else {
+                merge_chunk(ca, lo, hi, sv[q], dv[q]);
+                *reinterpret_cast<uint4*>(p.dst + ca) = make_uint4(dv[q][0], dv[q][1], dv[q][2], dv[q][3]);
+            }
+        }
+        if (sin && p.out_len) p.out_len[i] = len;  // (0 when not parsed; after the chunks' loads)
+        for (uint64_t q2 = __ballot(sin && md == 2u); q2; q2 &= q2 - 1) {  // uniform
+            const uint32_t kk = (uint32_t)__builtin_ctzll(q2);
+            tv_gather(p, i0 + kk, s_o[wv][kk], s_o[wv][kk], s_l[wv][kk] & 0x3FFFFFFFu, lane);
+        }
+        // all 64 began before the window's end: the next 64 may too
+        return ((__ballot(o < we) >> 63) & 1ull) != 0;
+    };
+    if (i0 >= p.b.n) return;
+    for (bool more = batch(i0); more && i0 + 64 < p.b.n; more = batch(i0)) {  // uniform
+        i0 += 64;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
@@ -969,24 +1144,55 @@ int pkt_to_vec_batch(pkt_ctx_t* ctx, const pkt_batch_t* b, const pkt_out_t* pars
     tp.dst_offsets = dst_offsets;
     tp.out_len = out_len;
     tp.overlap = nullptr;
+    tp.epoch = 0;
+    tp.win = false;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (PKTGPU_TOVEC_RMW && !dst_offsets && b->offsets && b->lens && b->n > 1) {
+    if (!dst_offsets && b->offsets && b->lens && b->n > 1 && b->n < 0xFFFFFFFFull && b->slab_len) {
         // does any 16-byte chunk hold bytes of two records?  (one pass over the index: 12 B/record)
         if (!ctx->tv_flag &&
-            (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), pkt_ctx::kTvFlags * sizeof(uint32_t))) != hipSuccess)
+            (e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_flag), pkt_ctx::kTvFlags * pkt_ctx::kTvSlotWords * sizeof(uint32_t))) != hipSuccess)
             return hip_fail(ctx, e, "hipMalloc (to_vec flag)");
+        uint32_t ep = ctx->tv_epoch + 1;
+        ep = ep ? ep : 1;
+        if (ep == 1) {  // first call, or 2^32 calls on: no word may hold the epochs to come
+            if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(ctx, e, "hipDeviceSynchronize");
+            if ((e = hipMemset(ctx->tv_flag, 0, pkt_ctx::kTvFlags * pkt_ctx::kTvSlotWords * sizeof(uint32_t))) != hipSuccess)
+                return hip_fail(ctx, e, "hipMemset (to_vec flag)");
+        }
+        ctx->tv_epoch = ep;
         const uint32_t slot = ctx->tv_next++ % pkt_ctx::kTvFlags;
-        uint32_t* flag = ctx->tv_flag + slot;
+        uint32_t* flag = ctx->tv_flag + slot * pkt_ctx::kTvSlotWords;
         hipEvent_t& ev = ctx->tv_ev[slot];
         if (!ev && (e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess)
             return hip_fail(ctx, e, "hipEventCreate (to_vec flag)");
         // the word's previous user (a call 256 calls ago, maybe on another stream) has read it
         if ((e = hipStreamWaitEvent(s, ev, 0)) != hipSuccess) return hip_fail(ctx, e, "hipStreamWaitEvent");
-        if ((e = hipMemsetAsync(flag, 0, sizeof(uint32_t), s)) != hipSuccess) return hip_fail(ctx, e, "hipMemsetAsync");
-        hipLaunchKernelGGL(tv_overlap_kernel, dim3((unsigned)((b->n - 1 + 255) / 256)), dim3(256), 0, s, b->offsets,
-                           b->lens, b->n, flag);
+        // the window table: first[w] per 4 KiB window of the slab (records indexed by u32)
+        const uint64_t nwin = (b->slab_len + kTvWin - 1) / kTvWin;
+        if (!ctx->tv_win_ev && (e = hipEventCreateWithFlags(&ctx->tv_win_ev, hipEventDisableTiming)) != hipSuccess)
+            return hip_fail(ctx, e, "hipEventCreate (to_vec windows)");
+        if (nwin > ctx->tv_win_cap) {
+            if (ctx->tv_win) {
+                if ((e = hipEventSynchronize(ctx->tv_win_ev)) != hipSuccess) return hip_fail(ctx, e, "hipEventSynchronize");
+                (void)hipFree(ctx->tv_win);
+                ctx->tv_win = nullptr, ctx->tv_win_cap = 0;
+            }
+            if ((e = hipMalloc(reinterpret_cast<void**>(&ctx->tv_win), nwin * sizeof(uint32_t))) != hipSuccess)
+                return hip_fail(ctx, e, "hipMalloc (to_vec windows)");
+            ctx->tv_win_cap = nwin;
+        }
+        // the previous call's window kernel has read the table
+        if ((e = hipStreamWaitEvent(s, ctx->tv_win_ev, 0)) != hipSuccess) return hip_fail(ctx, e, "hipStreamWaitEvent");
+        hipLaunchKernelGGL(tv_overlap_kernel, dim3((unsigned)((b->n + 255) / 256)), dim3(256), 0, s, b->offsets,
+                           b->lens, b->n, flag, ctx->tv_epoch, ctx->tv_win, nwin, b->slab_len);
         if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "tv_overlap_kernel launch");
         tp.overlap = flag;
+        tp.epoch = ctx->tv_epoch;
+        tp.win = true;
+        hipLaunchKernelGGL(tv_window_kernel, dim3((unsigned)((nwin + kRwBlock / 64 - 1) / (kRwBlock / 64))),
+                           dim3(kRwBlock), 0, s, tp, (const uint32_t*)ctx->tv_win, nwin);
+        if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "tv_window_kernel launch");
+        if ((e = hipEventRecord(ctx->tv_win_ev, s)) != hipSuccess) return hip_fail(ctx, e, "hipEventRecord");
     }
     hipLaunchKernelGGL(to_vec_kernel, dim3(grid_of(b->n)), dim3(kRwBlock), 0, reinterpret_cast<hipStream_t>(stream), tp);
     if ((e = hipGetLastError()) != hipSuccess) return hip_fail(ctx, e, "to_vec_kernel launch");

@@ -522,6 +522,74 @@ def test_to_vec_long_packets_both_chunk_maps_vs_oracle(P):
     assert (o[mask] == 0xEE).all()
 
 
+@pytest.mark.parametrize("layout", ["capture", "lead_gap_exact_dst", "dense_windows", "far_gap"])
+def test_to_vec_capture_windows_vs_oracle(P, layout):
+    """to_vec into a capture's own layout goes by destination window (4 KiB per wave, the records'
+    starts mapped per window): C4 records, Q2 GRE packets (list order != wire order, gathered by the
+    window holding their start), truncated records (nothing written, out_len 0) and 1.4 KB records
+    crossing windows, with 16-byte record headers between them.  Layouts: a pcap (24-byte global
+    header first); a 100 KB lead before the first record and a destination ending at the last
+    record's last byte (its final 16-byte chunk partial); > 64 records starting in one window (36-byte
+    records: the window takes them 64 at a time); one gap of 600 KB (a record spanning more than the
+    window table allows: to_vec_kernel takes the batch).  Each equals the oracle's
+    slow::parse(..).to_vec() (tests/lib.rs:790-802) and no other destination byte changes."""
+    inner = gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                  "1.1.1.1", "2.2.2.2", 0, 64, 0, 0, [], 53, 1000, False, b"x" * 8)
+    inner.remove(0)
+    q2 = [gen.create_gre_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5, "3.3.3.3", "4.4.4.4",
+                                0, 64, 0, 0, [], c, 0, k, s, 0, 0, 0, 0x1111, 0x2222, 0x33333333, 0x44444444,
+                                b"", inner).to_vec() for c, k, s in ((1, 1, 1), (1, 0, 1), (0, 1, 1), (1, 1, 0))]
+    rng = np.random.default_rng(len(layout))
+    s4, o4, l4 = gen.gen_c4(6000, seed=90 + len(layout))
+    pk = []
+    for i in range(6000):
+        r = rng.random()
+        if r < 0.03:
+            pk.append(q2[int(rng.integers(0, 4))])
+        elif layout == "dense_windows" and r < 0.6:
+            pk.append(q2[0][:20] if r < 0.3 else bytes(s4[int(o4[i]):int(o4[i]) + 20]))  # 36-byte records
+        elif r < 0.05:
+            pk.append(bytes(s4[int(o4[i]):int(o4[i]) + int(rng.integers(1, 40))]))
+        elif r < 0.07:
+            pk.append(gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5, "1.1.1.1",
+                                            "2.2.2.2", 0, 64, 0, 0, [], 7, 9, False, bytes(1400 - i % 13)).to_vec())
+        else:
+            pk.append(bytes(s4[int(o4[i]):int(o4[i]) + int(l4[i])]))
+    n = len(pk)
+    lens = np.array([len(x) for x in pk], np.uint64)
+    gaps = np.full(n, 16, np.uint64)
+    gaps[0] = {"capture": 40, "lead_gap_exact_dst": 100_000, "dense_windows": 40, "far_gap": 40}[layout]
+    if layout == "far_gap":
+        gaps[n // 2] = 600_000
+    offs = np.cumsum(gaps) + np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.uint64)
+    end = int(offs[-1] + lens[-1])
+    total = end if layout == "lead_gap_exact_dst" else end + 40
+    buf = rng.integers(0, 256, total, dtype=np.uint8)
+    for i, x in enumerate(pk):
+        buf[int(offs[i]):int(offs[i]) + len(x)] = np.frombuffer(x, np.uint8)
+    ds, do, dl = dev(buf), dev(offs), dev(lens.astype(np.uint32))
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst = torch.full((total,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst)
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    mask = np.ones(total, bool)
+    reordered = 0
+    for i, x in enumerate(pk):
+        try:
+            want = oracle.slow_parse_to_vec(x)
+        except ValueError:
+            assert ln[i] == 0, i
+            continue
+        a = int(offs[i])
+        assert ln[i] == len(want), i
+        assert o[a:a + len(want)].tobytes() == want, i
+        reordered += want != x
+        mask[a:a + len(want)] = False
+    assert reordered > 0
+    assert (o[mask] == 0xEE).all()
+
+
 # ------------------------------------------------------------------ mixed inputs
 def test_mixed_inputs_bit_exact(P):
     """The reference pcap, a C4 replay, C3/C2 slabs and random/truncated records under three
