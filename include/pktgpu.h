@@ -582,7 +582,9 @@ int pkt_gather_plan(uint64_t col_mask, int nshards, const uint64_t *n, const uin
  * device memory of `device` (the parse writes them) or all pinned host memory from pkt_host_alloc (each
  * step's columns are exported over the link while the next bytes copy in); step_bytes = new bytes that
  * start a step at a push (0 = 4 MiB).
- * push: append n bytes (host memory; the caller may reuse it when push returns).
+ * push: append n bytes (host memory; the caller may reuse it when push returns).  Pushes under 1 MiB
+ * are gathered in a pinned staging ring of the stream and copied in 1 MiB pieces (or earlier, when a
+ * step is due), without a wait per push; larger ones are copied from `bytes` and waited for.
  * poll: a step over the bytes not yet indexed, then wait: *n_records = the records wholly inside the
  * bytes so far (a record running past them is not an error yet), their columns written; offsets / lens
  * (HOST, [cap], may be NULL) receive their (data offset, incl_len).

@@ -1815,6 +1815,19 @@ struct pkt_pcap_stream {
     uint64_t step = 0;  // bytes of new data that start a step at a push
     bool done = false;
     std::string err;
+    // Pushes below kStageMax bytes are gathered in a pinned staging ring (host memcpy) and copied in
+    // by the slot, so push returns without waiting for a copy (a wait per push is ~20 us: 64 KiB
+    // pushes ran at 3.2 GB/s, r06z4; staged 16.6, r06z6); larger pushes are copied from the caller's
+    // buffer directly and waited for (195 MB in pushes of 256 KiB: 17.6 ms direct, 8.3 staged; 512 KiB
+    // direct 11.2; 1 MiB direct 7.7).  A slot is refilled once its copy has landed (stage_ev).
+    static constexpr uint32_t kStageSlots = 4;
+    static constexpr uint64_t kStageSlot = 1ull << 20;
+    static constexpr uint64_t kStageMax = 1ull << 20;
+    uint8_t* stage = nullptr;  // pinned, kStageSlots x kStageSlot
+    hipEvent_t stage_ev[kStageSlots] = {};
+    bool stage_used[kStageSlots] = {};
+    uint32_t cur = 0;   // the slot being filled
+    uint64_t fill = 0;  // its bytes
 };
 
 namespace {
@@ -1824,6 +1837,19 @@ int st_fail(pkt_pcap_stream* st, int code, const std::string& msg) {
     return code;
 }
 int st_ctx_fail(pkt_pcap_stream* st, int code) { return st_fail(st, code, st->ctx ? st->ctx->err : "ctx"); }
+// The staged bytes of the current slot to the device (in order with every earlier copy: one copy stream).
+int st_flush(pkt_pcap_stream* st) {
+    if (!st->fill) return PKT_SUCCESS;
+    const uint32_t c = st->cur;
+    int rc = ingest_copy(st->ig, st->stage + (uint64_t)c * pkt_pcap_stream::kStageSlot, st->fill);
+    if (rc != PKT_SUCCESS) return rc;
+    const hipError_t e = hipEventRecord(st->stage_ev[c], st->ctx->hp.s[1]);
+    if (e != hipSuccess) return ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventRecord (staging)"));
+    st->stage_used[c] = true;
+    st->cur = (c + 1) % pkt_pcap_stream::kStageSlots;
+    st->fill = 0;
+    return PKT_SUCCESS;
+}
 }  // namespace
 
 extern "C" {
@@ -1851,6 +1877,14 @@ int pkt_pcap_stream_open(int device, uint64_t max_bytes, uint64_t cap, int entry
     }
     st->max_bytes = max_bytes;
     st->step = step_bytes ? step_bytes : kStreamStep;
+    hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->stage), pkt_pcap_stream::kStageSlots * pkt_pcap_stream::kStageSlot, 0);
+    for (uint32_t k = 0; k < pkt_pcap_stream::kStageSlots && e == hipSuccess; k++)
+        e = hipEventCreateWithFlags(&st->stage_ev[k], hipEventDisableTiming);
+    if (e != hipSuccess) {
+        rc = hip_fail(st->ctx, e, "pinned staging ring");
+        pkt_pcap_stream_close(st);
+        return rc;
+    }
     *out_st = st;
     return PKT_SUCCESS;
 }
@@ -1858,13 +1892,36 @@ int pkt_pcap_stream_open(int device, uint64_t max_bytes, uint64_t cap, int entry
 int pkt_pcap_stream_push(pkt_pcap_stream_t* st, const uint8_t* bytes, uint64_t n) {
     if (!st || (n && !bytes)) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
     if (st->done) return st_fail(st, PKT_ERR_INVALID_ARG, "the capture is finished");
-    if (n > st->max_bytes - st->ig.hi) return st_fail(st, PKT_ERR_INVALID_ARG, "push past the capture's max_bytes");
+    if (n > st->max_bytes - st->ig.hi - st->fill) return st_fail(st, PKT_ERR_INVALID_ARG, "push past the capture's max_bytes");
     if (!n) return PKT_SUCCESS;
-    int rc = ingest_copy(st->ig, bytes, n);
-    // the caller may reuse its buffer once this returns
-    const hipEvent_t landed = rc == PKT_SUCCESS ? ingest_copied(st->ig, st->ig.hi) : nullptr;
-    const hipError_t e = landed ? hipEventSynchronize(landed) : hipSuccess;
-    if (e != hipSuccess) rc = ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventSynchronize (push)"));
+    if (st->ig.rc != PKT_SUCCESS) return st_ctx_fail(st, st->ig.rc);
+    int rc = PKT_SUCCESS;
+    // the caller may reuse its buffer once this returns: its bytes are staged, or their copy has landed
+    if (n < pkt_pcap_stream::kStageMax) {
+        while (n && rc == PKT_SUCCESS) {
+            const uint32_t c = st->cur;
+            if (!st->fill && st->stage_used[c]) {  // the slot's previous copy must have landed
+                const hipError_t e = hipEventSynchronize(st->stage_ev[c]);
+                if (e != hipSuccess) rc = ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventSynchronize (staging)"));
+                st->stage_used[c] = false;
+            }
+            const uint64_t take = std::min(n, pkt_pcap_stream::kStageSlot - st->fill);
+            if (rc == PKT_SUCCESS) std::memcpy(st->stage + (uint64_t)c * pkt_pcap_stream::kStageSlot + st->fill, bytes, take);
+            st->fill += take;
+            bytes += take;
+            n -= take;
+            if (rc == PKT_SUCCESS && st->fill == pkt_pcap_stream::kStageSlot) rc = st_flush(st);
+        }
+        // a step is due: its bytes go now (steps run over copied bytes)
+        const uint64_t have = st->ig.hi + st->fill;
+        if (rc == PKT_SUCCESS && have >= 24 && have - st->ig.indexed >= st->step) rc = st_flush(st);
+    } else {
+        rc = st_flush(st);  // the staged bytes first: the file's order
+        if (rc == PKT_SUCCESS) rc = ingest_copy(st->ig, bytes, n);
+        const hipEvent_t landed = rc == PKT_SUCCESS ? ingest_copied(st->ig, st->ig.hi) : nullptr;
+        const hipError_t e = landed ? hipEventSynchronize(landed) : hipSuccess;
+        if (e != hipSuccess) rc = ingest_fail(st->ig, hip_fail(st->ctx, e, "hipEventSynchronize (push)"));
+    }
     if (rc == PKT_SUCCESS && st->ig.hi >= 24 && st->ig.hi - st->ig.indexed >= st->step) rc = ingest_step(st->ig, false);
     return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);
 }
@@ -1872,8 +1929,9 @@ int pkt_pcap_stream_push(pkt_pcap_stream_t* st, const uint8_t* bytes, uint64_t n
 int pkt_pcap_stream_poll(pkt_pcap_stream_t* st, uint64_t* n_records, uint64_t* offsets, uint32_t* lens) {
     if (!st || !n_records) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
     *n_records = 0;
+    int rc = st->done ? PKT_SUCCESS : st_flush(st);
+    if (rc != PKT_SUCCESS) return st_ctx_fail(st, rc);
     if (st->ig.hi < 24) return st->ig.rc;  // not even the global header yet
-    int rc = PKT_SUCCESS;
     if (!st->done && st->ig.hi > st->ig.indexed) rc = ingest_step(st->ig, false);
     if (rc == PKT_SUCCESS) rc = ingest_wait(st->ig, n_records, offsets, lens);
     return rc == PKT_SUCCESS ? rc : st_ctx_fail(st, rc);
@@ -1882,8 +1940,9 @@ int pkt_pcap_stream_poll(pkt_pcap_stream_t* st, uint64_t* n_records, uint64_t* o
 int pkt_pcap_stream_finish(pkt_pcap_stream_t* st, uint64_t* n_records, uint64_t* offsets, uint32_t* lens) {
     if (!st || !n_records) return st_fail(st, PKT_ERR_INVALID_ARG, "null argument");
     *n_records = 0;
+    int rc = st->done ? PKT_SUCCESS : st_flush(st);
+    if (rc != PKT_SUCCESS) return st_ctx_fail(st, rc);
     if (st->ig.hi < 24) return st_fail(st, PKT_ERR_INVALID_ARG, "pcap shorter than its global header");
-    int rc = PKT_SUCCESS;
     if (!st->done) rc = ingest_step(st->ig, true);  // the tail as pkt_pcap_index takes it (errors included)
     st->done = true;
     if (rc == PKT_SUCCESS) rc = ingest_wait(st->ig, n_records, offsets, lens);
@@ -1896,7 +1955,10 @@ const char* pkt_pcap_stream_last_error(const pkt_pcap_stream_t* st) { return st 
 
 int pkt_pcap_stream_close(pkt_pcap_stream_t* st) {
     if (!st) return PKT_SUCCESS;
-    if (st->ctx) pkt_ctx_destroy(st->ctx);  // waits for its streams
+    if (st->ctx) pkt_ctx_destroy(st->ctx);  // waits for its streams (the staging ring's copies too)
+    for (hipEvent_t ev : st->stage_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (st->stage) (void)hipHostFree(st->stage);
     delete st;
     return PKT_SUCCESS;
 }
