@@ -307,7 +307,7 @@ __global__ __launch_bounds__(256) void tv_overlap_kernel(const uint64_t* __restr
     bool bad = false;
     if (i < n) {
         const uint64_t o1 = offs[i], e1 = o1 + lens[i];
-        bad = e1 > slab_len;
+        bad = e1 > slab_len || lens[i] == 0;  // (an empty record has no window to write its out_len)
         if (i == 0 || i == n - 1) reinterpret_cast<uint64_t*>(flag + 2)[i == 0 ? 0 : 1] = e1;
         if (i >= 1) {
             const uint64_t o0 = offs[i - 1], l0 = lens[i - 1], e0 = o0 + l0;

@@ -590,6 +590,35 @@ def test_to_vec_capture_windows_vs_oracle(P, layout):
     assert (o[mask] == 0xEE).all()
 
 
+def test_to_vec_capture_empty_last_record_at_a_window_start(P):
+    """A capture-layout batch whose last record is empty and starts exactly at a 4 KiB boundary: an
+    empty record sends the batch to to_vec_kernel (the window path would have no window to write its
+    out_len); every out_len (0 for the empty record) and every to_vec equals the oracle."""
+    s4, o4, l4 = gen.gen_c4(200, seed=123)
+    pk = [bytes(s4[int(o4[i]):int(o4[i]) + int(l4[i])]) for i in range(200)]
+    lens = np.array([len(x) for x in pk] + [0], np.uint64)
+    offs = np.zeros(len(lens), np.uint64)
+    offs[0] = 40
+    for i in range(1, len(lens) - 1):
+        offs[i] = offs[i - 1] + lens[i - 1] + np.uint64(16)
+    end = int(offs[-2] + lens[-2])
+    offs[-1] = np.uint64((end + 16 + 4095) // 4096 * 4096)
+    total = int(offs[-1]) + 64
+    buf = np.zeros(total, np.uint8)
+    for i, x in enumerate(pk):
+        buf[int(offs[i]):int(offs[i]) + len(x)] = np.frombuffer(x, np.uint8)
+    ds, do, dl = dev(buf), dev(offs), dev(lens.astype(np.uint32))
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst = torch.full((total,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst)
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    assert ln[-1] == 0
+    for i, x in enumerate(pk):
+        want = oracle.slow_parse_to_vec(x)
+        assert ln[i] == len(want) and o[int(offs[i]):int(offs[i]) + len(want)].tobytes() == want, i
+
+
 # ------------------------------------------------------------------ mixed inputs
 def test_mixed_inputs_bit_exact(P):
     """The reference pcap, a C4 replay, C3/C2 slabs and random/truncated records under three

@@ -27,7 +27,7 @@ def overlap_pass(offs, lens, slab_len):
     bad = False
     for i in range(n):
         o1, e1 = int(offs[i]), int(offs[i]) + int(lens[i])
-        bad |= e1 > slab_len
+        bad |= e1 > slab_len or int(lens[i]) == 0
         if i >= 1:
             o0, l0 = int(offs[i - 1]), int(lens[i - 1])
             e0 = o0 + l0
@@ -135,6 +135,9 @@ def test_overlap_pass_sends_unfit_batches_to_to_vec_kernel():
     past = lens.copy()
     past[-1] += slab_len  # past the slab's end
     assert overlap_pass(offs, past, slab_len)[0]
+    empty = lens.copy()
+    empty[-1] = 0  # an empty last record (its start may open a window past end(n-1)): to_vec_kernel
+    assert overlap_pass(offs, empty, slab_len)[0]
     far = offs.copy()
     far[300:] += np.uint64(2 * MAX_WIN * WIN)  # a gap of more than 128 windows
     assert overlap_pass(far, lens, int(far[-1] + lens[-1]) + 1)[0]
