@@ -684,7 +684,17 @@ def run_mgpu(args, ndev):
 
     c5 = None
     if args.config == "c2" and not args.no_c5:
-        c5 = run_c5_mgpu(args, torch, MP, per, cols, entry)
+        # (after the headline's timed region: a failure here, e.g. RCCL on a new node, is recorded in
+        # the line instead of losing it)
+        try:
+            c5 = run_c5_mgpu(args, torch, MP, per, cols, entry)
+        except Exception as ex:  # noqa: BLE001
+            c5 = {"workload": "C5", "error": f"{type(ex).__name__}: {ex}"}
+            print(f"bench.py: C5 record failed: {ex}", file=sys.stderr)
+            try:
+                MP.synchronize()
+            except Exception:  # noqa: BLE001
+                pass
 
     span = o0["payload_off"].cpu().numpy() if "payload_off" in o0 else np.full(n, 64, np.int64)
     read_b, write_b = algorithmic_bytes(n, cols, max(used_slots, 1), span)
