@@ -590,6 +590,59 @@ def test_to_vec_capture_windows_vs_oracle(P, layout):
     assert (o[mask] == 0xEE).all()
 
 
+@pytest.mark.parametrize("layout", ["packed", "gaps_shift", "truncated", "exact_end", "q2_fallback"])
+def test_to_vec_dst_layouts_in_order_vs_oracle(P, layout):
+    """to_vec into a destination layout of its own (dst_offsets), records in order: chunks holding the
+    end of one record and the start of the next (their source alignments differ).  Layouts: packed
+    back to back (the bench's); 1-9 byte gaps and an odd start; records truncated to 17-40 bytes (not
+    parsed: nothing written, their bytes left untouched); a destination ending at the last record's
+    last byte; a batch holding a Q2 GRE packet.  Every to_vec and out_len equals the oracle's
+    slow::parse(..).to_vec() (tests/lib.rs:790-802) and no other destination byte changes.  (Round 6
+    measured a by-window kernel for these layouts and kept to_vec_kernel: profiles/ab/r06zr_*.)"""
+    s4, o4, l4 = gen.gen_c4(30000, seed=70 + len(layout))
+    rng = np.random.default_rng(len(layout))
+    pk = [bytes(s4[int(o4[i]):int(o4[i]) + int(l4[i])]) for i in range(len(o4))]
+    if layout == "truncated":
+        for i in rng.choice(len(pk), 1500, replace=False):
+            pk[i] = pk[i][:int(rng.integers(17, 41))]
+    if layout == "q2_fallback":
+        inner = gen.create_udp_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5,
+                                      "1.1.1.1", "2.2.2.2", 0, 64, 0, 0, [], 53, 1000, False, b"x" * 8)
+        inner.remove(0)
+        pk[777] = gen.create_gre_packet("00:01:02:03:04:05", "00:06:07:08:09:0a", False, 0, 0, 5, "3.3.3.3",
+                                        "4.4.4.4", 0, 64, 0, 0, [], 1, 0, 1, 1, 0, 0, 0, 0x1111, 0x2222,
+                                        0x33333333, 0x44444444, b"", inner).to_vec()
+    n = len(pk)
+    lens = np.array([len(x) for x in pk], np.uint64)
+    offs = np.concatenate([[0], np.cumsum(lens + np.uint64(16))[:-1]]).astype(np.uint64) + np.uint64(40)
+    buf = np.zeros(int(offs[-1] + lens[-1]) + 64, np.uint8)
+    for i, x in enumerate(pk):
+        buf[int(offs[i]):int(offs[i]) + len(x)] = np.frombuffer(x, np.uint8)
+    gaps = rng.integers(1, 10, n).astype(np.uint64) if layout == "gaps_shift" else np.zeros(n, np.uint64)
+    start = np.uint64(5 if layout == "gaps_shift" else 0)
+    doff = np.concatenate([[0], np.cumsum(lens + gaps)[:-1]]).astype(np.uint64) + start
+    end = int(doff[-1] + lens[-1])
+    dst_len = end if layout == "exact_end" else end + 100
+    ds, do, dl = dev(buf), dev(offs), dev(lens.astype(np.uint32))
+    res = P.parse(ds, offsets=do, lens=dl, columns=["chain"])
+    dst = torch.full((dst_len,), 0xEE, dtype=torch.uint8, device="cuda")
+    out, ln = P.to_vec(ds, res, offsets=do, lens=dl, dst=dst, dst_offsets=dev(doff))
+    torch.cuda.synchronize()
+    o, ln = out.cpu().numpy(), ln.cpu().numpy()
+    mask = np.ones(dst_len, bool)
+    for i, x in enumerate(pk):
+        try:
+            want = oracle.slow_parse_to_vec(x)
+        except ValueError:
+            assert ln[i] == 0, i
+            continue
+        a = int(doff[i])
+        assert ln[i] == len(want), i
+        assert o[a:a + len(want)].tobytes() == want, i
+        mask[a:a + len(want)] = False
+    assert (o[mask] == 0xEE).all()
+
+
 def test_to_vec_capture_empty_last_record_at_a_window_start(P):
     """A capture-layout batch whose last record is empty and starts exactly at a 4 KiB boundary: an
     empty record sends the batch to to_vec_kernel (the window path would have no window to write its
