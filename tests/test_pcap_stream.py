@@ -106,6 +106,17 @@ def test_c4_random_push_sizes(step, pinned):
     _run(buf, sizes, step, pinned=pinned)
 
 
+def test_staged_and_direct_pushes_interleaved():
+    """Pushes under 1 MiB go through the stream's pinned staging ring, larger ones are copied directly
+    (include/pktgpu.h): a C4 capture pushed as small / 1 MiB / 2-3 MiB / tiny pieces in turn, with
+    steps of 256 KiB and polls between, must keep the bytes in order (staged bytes flushed before a
+    direct copy) and give the host indexer's records and the oracle's columns."""
+    buf, _, _ = gen.gen_c4(40_000, seed=808)
+    sizes = [70_000, 1 << 20, 5, (2 << 20) + 333, 123_457, 1, (1 << 20) - 1, (3 << 20) + 7, 64, 999_999]
+    _run(buf, sizes, 256 << 10)
+    _run(buf, sizes[::-1], 0, pinned=True)
+
+
 def test_long_records_and_fake_chains():
     """Records up to 70 KB (many steps of 4 KiB pass inside one record), payloads that are themselves
     chains of plausible record headers, zero-filled payloads; pushed in 3000-byte pieces with a step per
