@@ -592,6 +592,42 @@ def host_pcap_record(P, n=1 << 20, reps=5):
                                   "wall clock over all captures / captures"}}
 
 
+def pcap_stream_record(P, n=1 << 20, reps=3, pushes=(1 << 20, 64 << 10)):
+    """north_star's "NIC ring buffer" form of the capture path (tests/pcap.rs:7-37 as bytes arrive):
+    the C4 capture in pinned host memory pushed into pkt_pcap_stream_* in pieces of `push` bytes (each
+    push returns with the caller's bytes reusable), 4 MiB steps, finish; device columns.  Wall clock
+    from the first push to finish's return, median of reps; the record count is checked."""
+    from pktgpu import gen
+    from pktgpu.stream import PcapStream
+    buf, _, _ = gen.gen_c4(n, seed=0x5EED0007)
+    hb = P.host_empty((buf.size,), np.uint8)
+    hb[:] = buf
+    rows = {}
+    ok = True
+    for push in pushes:
+        ts = []
+        for r in range(reps + 1):  # (the first: warm)
+            st = PcapStream(0, max_bytes=buf.size + 64, cap=n, columns="all")
+            try:
+                t0 = time.perf_counter()
+                for p0 in range(0, buf.size, push):
+                    st.push(hb[p0:p0 + push])
+                c, _ = st.finish(index=False)
+                if r:
+                    ts.append(time.perf_counter() - t0)
+                ok &= c == n
+            finally:
+                st.close()
+        t = float(np.median(ts))
+        rows[str(push)] = {"ms_per_capture": round(t * 1e3, 4), "Grecords/s": round(n / t / 1e9, 4),
+                           "host_to_device_GB/s": round(buf.size / t / 1e9, 2)}
+    return {"workload": f"C4 capture: {n} records, {buf.size} B in pinned host memory, pushed as it would arrive",
+            "entry": "pkt_pcap_stream_open / _push (pieces of push_bytes; under 1 MiB through the stream's pinned "
+                     "staging ring) / _finish, 4 MiB steps, all 49 columns into device memory",
+            "by_push_bytes": rows, "count_ok": bool(ok), "reps": reps,
+            "timing": "wall clock from the first push to finish's return, median"}
+
+
 # ------------------------------------------------------------------------------ the library's multi-GPU entry
 def run_mgpu(args, ndev):
     """One process, ndev devices through pkt_mgpu (the measured form for every N)."""
@@ -760,6 +796,7 @@ def run_mgpu(args, ndev):
         res["host"] = host_record(P, torch, cols)
         res["pcap"] = pcap_record(P, torch, MP.torch_devices[0])
         res["host_pcap"] = host_pcap_record(P)
+        res["pcap_stream"] = pcap_stream_record(P)
     if ndev == 1 and not args.no_cpu_baseline:
         cores, aff, quota = host_cores()
         threads = args.cpu_threads or cores
